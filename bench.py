@@ -1,0 +1,237 @@
+#!/usr/bin/env python3
+"""Langevin-step throughput of the fused PSGLA+TV HIP step (BASELINE.json configs[1]).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 64] [--scaling weak|strong]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Workload (config.workload): PSGLA, inpainting 50 %, TV denoiser (deepinv TVDenoiser,
+n_it_max=10, warm-started), s = 10/255, lambda = 10, delta = s^2, sigma = 1/255,
+n_inter = n_inter_mmse = 10 (the N = 10000 TV settings of sampling_images.py:180-198),
+synthetic 3x256x256 fp32 images (one per chain, U[0,1) from Philox seed 1234 + chain id),
+the reference's shared inpainting mask (torch.rand on the device generator, seed_ip = 0,
+> 0.5).  64 chains per GPU (weak scaling: chains are independent, no collective in the
+step; chain ids are global so results do not depend on the GPU count); one RCCL
+all_reduce after the timed region combines the per-chain MMSE PSNR.
+
+Timed region: K steps replayed from a hipGraph (the device step counter advances the noise
+counter, block-mean coefficients and sample / block slots), barrier + synchronize on both
+sides, max over ranks.  value = chain-steps (image-steps of 3x256x256) per second over all
+GPUs.  The dominant kernel (tv_main_kernel) is also timed alone with HIP events on its own
+stream for the roofline figure.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "Langevin steps/sec (3×256×256, batch=64) at 1/2/4/8 GPU; HBM GB/s vs roofline"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=400)
+    p.add_argument("--warmup", type=int, default=40)
+    p.add_argument("--batch", type=int, default=64, help="chains per GPU (weak) or in total (strong)")
+    p.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    p.add_argument("--H", type=int, default=256)
+    p.add_argument("--W", type=int, default=256)
+    p.add_argument("--graph-steps", type=int, default=20)
+    p.add_argument("--exact", action="store_true", help="bit-exact (IEEE div/sqrt) TV kernel")
+    p.add_argument("--kernel-iters", type=int, default=50)
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r01_pmc_tv_main.json"))
+    return p.parse_args()
+
+
+def algorithmic_bytes_per_launch(B, C, H, W, step0, steps, n_inter, nm):
+    """Compulsory HBM bytes of one tv_main_kernel launch, averaged over the timed steps.
+    Per element: read X 4 + u2 8 + y 4 (+ mean 4 + sq 4 unless the block restarts), write
+    X 4 + u2 8 + mean 4 + sq 4 (block means instead of the live accumulators at a block
+    end), + the sample copy 4 every n_inter steps; + the (H,W) u8 mask once per launch."""
+    E = B * C * H * W
+    tot = 0.0
+    per = nm + 1
+    for i in range(step0, step0 + steps):
+        b = 4 + 8 + 4 + 4 + 8 + 8       # X r/w, u2 r/w, y r, mean+sq w (or block w)
+        if i % per != 0:
+            b += 8                       # mean + sq read
+        if i % n_inter == 0:
+            b += 4                       # sample store
+        tot += b * E + H * W
+    return tot / steps
+
+
+def cpu_baseline(seconds: float):
+    """The reference algorithm on the host cores: oracle/ (op-for-op torch-CPU restatement of
+    restoration_algorithms.py:231-271 + the deepinv TV prox), batch 1 as the reference runs."""
+    from oracle import psgla_oracle as orc
+    threads = torch.get_num_threads()
+    g = torch.Generator().manual_seed(1234)
+    x = torch.rand((1, 3, 256, 256), generator=g)
+    dg, y, init, _ = orc.inpainting_problem(x, seed_ip=0)
+    s = 10 / 255.0
+    tv = orc.TVDenoiser(n_it_max=10)
+    # time a bounded number of steps: run blocks of 10 steps until `seconds` have elapsed
+    steps = 0
+    t0 = time.perf_counter()
+    X = init
+    alpha = torch.tensor(1.0)
+    lam = torch.tensor(10.0)
+    while True:
+        Xl, _, _ = orc.psgla(X, dg, tv, alpha, lam, sig_float=s, delta=s ** 2, n_iter=10, n_inter=10,
+                             n_inter_mmse=10, seed=0)
+        X = Xl[-1][None]
+        steps += 10
+        if time.perf_counter() - t0 > seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "image-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} PSGLA+TV steps, batch 1, 3x256x256, torch-CPU oracle, {threads} threads, "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
+    from psgla_for_posterior_sampling_amd.sharding import chain_range
+
+    C, H, W = 3, args.H, args.W
+    total_chains = args.batch * world if args.scaling == "weak" else args.batch
+    c0, c1 = chain_range(total_chains, world, rank)
+    B = c1 - c0
+    # synthetic per-chain ground truths, the reference's shared mask, observations
+    xs = torch.empty((B, C, H, W), device=dev)
+    for b in range(B):
+        g = torch.Generator(device=dev).manual_seed(1234 + c0 + b)
+        xs[b] = torch.rand((C, H, W), generator=g, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(0)
+    m = torch.rand((H, W), generator=gen, device=dev)
+    mask_2d = 1 * (m > 0.5)
+    mask = torch.ones(C, device=dev)[None, :, None, None] * mask_2d[None, None]
+    sigma1 = 1 / 255.0
+    y = mask * xs + torch.normal(torch.zeros_like(xs), std=sigma1 * torch.ones_like(xs), generator=gen)
+    init = mask * y + (1 - mask) * 0.5
+    s = 10 / 255.0
+    lam = 10.0
+    delta = s ** 2
+    c1f = float((torch.tensor(delta).float() / torch.tensor(lam).float()).item())
+    c2f = float((torch.tensor(np.sqrt(2)).float() * torch.tensor(s).float()).item())
+    n_inter = nm = 10
+    n_iter = args.warmup + args.steps
+    eng = FusedTvChains(init.contiguous(), y.contiguous(), mask_2d.to(torch.uint8), c1=c1f, c2=c2f,
+                        sigma2=float(np.float32(sigma1 ** 2)), alpha=1.0, ths=float(np.float32(s)),
+                        tv=K.TvConstants(n_it_max=10), seed=0, n_iter=n_iter + args.kernel_iters,
+                        n_inter=n_inter, n_inter_mmse=nm, chain0=c0, exact=args.exact)
+    gs = max(1, min(args.graph_steps, args.steps))
+    # warm-up: eager steps + graph capture
+    eng.step(max(1, args.warmup - gs))
+    eng.capture(gs)
+    eng.replay(1)
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    reps = args.steps // gs
+    steps = reps * gs
+    step0 = eng.steps_done
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.replay(reps)
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # ---- dominant kernel alone (HIP events on the launching stream) ----
+    ks = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(ks):
+        eng.launch_main_only(3)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(ks)
+        eng.launch_main_only(args.kernel_iters)
+        e1.record(ks)
+    e1.synchronize()
+    kern_ms = e0.elapsed_time(e1) / args.kernel_iters
+    alg_bytes = algorithmic_bytes_per_launch(B, C, H, W, step0, steps, n_inter, nm)
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+
+    # ---- final reduction (RCCL): per-chain MMSE PSNR of the blocks so far ----
+    from psgla_for_posterior_sampling_amd.sharding import reduce_psnr
+    blocks, _ = eng.blocks()
+    psnr_sum, n_chains = reduce_psnr(blocks, xs, world)
+
+    traffic = None
+    if os.path.exists(args.pmc_json):
+        try:
+            traffic = json.load(open(args.pmc_json)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        cpu = None if args.no_cpu else cpu_baseline(args.cpu_seconds)
+        value = total_chains * steps / dt
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "image-steps/s (chain-steps of 3x256x256, summed over GPUs)",
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": args.scaling,
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (U[0,1) images per chain, reference mask/observation recipe)",
+            "config": {"workload": "psgla+TV inpainting 50% (BASELINE configs[1]), n_it_max=10",
+                       "global_batch": total_chains, "chains_per_gpu": B, "image": [C, H, W],
+                       "parallelism": f"chains{world}", "graph_steps": gs,
+                       "kernel_mode": "exact" if args.exact else "fast",
+                       "batch_steps_per_s_per_gpu": round(steps / dt, 2)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "tv_main_kernel", "kernel_ms": round(kern_ms, 5),
+                         "algorithmic_bytes_per_launch": int(alg_bytes)},
+            "cpu_baseline": cpu,
+            "mmse_psnr_mean_db": round(psnr_sum / max(n_chains, 1), 3),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,166 @@
+/*
+ * psgla_hip.h -- C ABI of libpsgla_hip.so, the MI355X (gfx950) hot path of the
+ * PSGLA / PnP-ULA Langevin samplers of Marien-RENAUD/PSGLA-for-posterior-sampling.
+ *
+ * The reference is pure Python: its "interface" for this path is the pair of
+ * functions psgla(...) (restoration_algorithms.py:163) and pnpula(...) (:38) plus
+ * the closures they call.  Each entry point below replaces a named piece of that
+ * loop; the Python host package (psgla_for_posterior_sampling_amd) binds them with
+ * ctypes and keeps the reference's signatures (INTEGRATION.md shows the binding a
+ * maintainer would add to the reference itself).
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a DEVICE pointer the caller owns (PyTorch caching allocator);
+ *     the library never allocates, frees or synchronises;
+ *   - `stream` is a hipStream_t passed as void*; every launch is asynchronous on it,
+ *     so the calls are legal inside hipGraph / torch.cuda.graph capture;
+ *   - tensors are fp32 NCHW contiguous, one chain per batch entry: (B, C, H, W);
+ *     the TV dual is (B, C, H, W, 2) as in deepinv's TVDenoiser;
+ *   - the step index i of the Langevin loop is read from `*d_step + step_offset`
+ *     when d_step != NULL (device counter, for graph replay), else it is
+ *     `step_offset`;
+ *   - return 0 on success or a hipError_t value; psgla_last_error() describes the
+ *     last failure of the calling thread.  Nothing throws across the ABI.
+ */
+#ifndef PSGLA_HIP_H_
+#define PSGLA_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSGLA_HIP_ABI_VERSION 1
+
+/* Max inner TV iterations the fused (temporally blocked) kernel handles. */
+#define PSGLA_TV_MAX_FUSED_IT 24
+
+int psgla_abi_version(void);
+const char* psgla_last_error(void);
+
+/* ---------------------------------------------------------------------------------
+ * Sample storage and running mean / second moment
+ *   reference: restoration_algorithms.py:240-244 (samples every n_inter steps) and
+ *   :255-271 (online block means of X and X^2; a block holds n_inter_mmse+1 samples,
+ *   the trailing partial block is dropped).  Step i uses acc_coef[i mod (nm+1)] =
+ *   (fp32(k/(k+1)), fp32(1/(k+1))); the block index is i / (nm+1).
+ * ------------------------------------------------------------------------------- */
+typedef struct PsglaSchedule {
+    int64_t* d_step;          /* device step counter, or NULL (then step_offset is the step) */
+    int64_t step_offset;
+    int32_t n_inter;          /* X stored when i % n_inter == 0; <= 0: never            */
+    int32_t n_inter_mmse;     /* < 0: no accumulation                                    */
+    const float* acc_coef;    /* device [(n_inter_mmse+1) * 2]                           */
+    float* samples;           /* [samples_cap][B][C][H][W] or NULL                       */
+    int64_t samples_cap;
+    float* blocks;            /* [blocks_cap][B][C][H][W] block means of X               */
+    float* blocks2;           /* [blocks_cap][B][C][H][W] block means of X^2             */
+    int64_t blocks_cap;
+} PsglaSchedule;
+
+/* ---------------------------------------------------------------------------------
+ * psgla_tv_step: ONE fused PSGLA Langevin step with the inpainting fidelity and the
+ * warm-started TV prox, for B chains.  Replaces one iteration of
+ *   restoration_algorithms.py:231-271 with
+ *   data_grad = sampling_images.py:295  (-mask*(x - y)/sigma2)
+ *   denoiser  = deepinv 0.2.1 TVDenoiser(n_it_max) (sampling_images.py:138), ths = s
+ * i.e.  Z ~ N(0,1);  Y = (X + c1*g(X)) + c2*Z;  X' = (1-alpha)*Y + alpha*TVprox(Y);
+ *       accumulators / samples per PsglaSchedule.
+ * State is double-buffered by step parity: step i reads x[i&1], u2[i&1], ...
+ * and writes x[(i+1)&1], ...  Two kernels are launched: the fused tile kernel and
+ * a small finaliser that honours deepinv's early stop (rel_err < tol at inner
+ * iteration k >= 2, per chain: the affected chains are recomputed with k+1 inner
+ * iterations), clears `fresh` and advances *d_step.
+ * ------------------------------------------------------------------------------- */
+typedef struct PsglaTvStep {
+    int32_t B, C, H, W;
+    float* x[2];              /* chain state X (B,C,H,W)                                */
+    float* u2[2];             /* TV dual (B,C,H,W,2)                                    */
+    float* x2[2];             /* TV primal when alpha != 1; NULL when alpha == 1 (x2==X)*/
+    float* mean[2];           /* live block accumulators (B,C,H,W); NULL if no accum    */
+    float* sq[2];
+    const float* y;           /* observation (B,C,H,W); chain stride y_chain_stride     */
+    int64_t y_chain_stride;   /* elements; 0 = one observation shared by all chains     */
+    const uint8_t* mask;      /* inpainting mask (H,W) per chain, 1 = observed          */
+    int64_t mask_chain_stride;/* bytes; 0 = shared                                       */
+    float c1;                 /* fp32(delta)/fp32(lambd)    (restoration_algorithms.py:236) */
+    float c2;                 /* fp32(sqrt 2) * fp32(s)     (:228, :236)                  */
+    float sigma2;             /* fp32(sigma1^2), used as a divisor (sampling_images.py:295) */
+    float alpha;              /* relaxation (:238)                                        */
+    float tau, one_plus_tau, sigma_tv, rho, ths, tol;  /* TVDenoiser constants (fp32)     */
+    int32_t n_tv;             /* inner iterations n_it_max (<= PSGLA_TV_MAX_FUSED_IT)     */
+    int32_t exact;            /* 1: reference op order + IEEE div/sqrt (bit-exact checker mode) */
+    uint64_t seed;            /* seed_alg                                                 */
+    int32_t chain0;           /* global id of chain 0 of this batch (multi-GPU sharding)  */
+    int32_t advance_step;     /* 1: finaliser increments *d_step                           */
+    int32_t* fresh;           /* device int: 1 -> TV restart (x2=Y, u2=0), cleared after the step */
+    double* norms;            /* device [B][n_tv][2], zero-initialised (rel_err partial sums) */
+    int32_t* arrive;          /* device int, zero-initialised (finaliser arrival counter)   */
+    int32_t launch_mask;      /* 0 or 3: both kernels; 1: tile kernel only (re-runs the same step:
+                                 idempotent, for kernel timing); 2: finaliser only            */
+} PsglaTvStep;
+
+int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * psgla_tv_prox: TVDenoiser.forward(y, ths) on a (B,C,H,W) tensor, deepinv 0.2.1
+ * semantics: warm start from (x2_in, u2_in) unless `fresh`; early stop on the
+ * relative change of the WHOLE tensor (as deepinv computes it).  Outputs x2_out,
+ * u2_out (new buffers, like deepinv's out-of-place updates).
+ * ------------------------------------------------------------------------------- */
+typedef struct PsglaTvProx {
+    int32_t B, C, H, W;
+    const float* y;
+    const float* x2_in;  const float* u2_in;   /* ignored when fresh                      */
+    float* x2_out;       float* u2_out;
+    float tau, one_plus_tau, sigma_tv, rho, ths, tol;
+    int32_t n_tv, exact, fresh;
+    double* norms;            /* device [n_tv][2], zeroed */
+    int32_t* arrive;          /* device int, zeroed       */
+} PsglaTvProx;
+
+int psgla_tv_prox(const PsglaTvProx* d, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Generic (opaque-closure) building blocks.
+ * ------------------------------------------------------------------------------- */
+/* out[b][e] = N(0,1) of "psgla noise v1" (seed, chain0+b, step, tag);  torch.randn at
+ * restoration_algorithms.py:232 / :104 */
+int psgla_normal_fill(float* out, int32_t B, int64_t E, uint64_t seed, int32_t chain0,
+                      const int64_t* d_step, int64_t step_offset, uint32_t tag, void* stream);
+
+/* Y = (X + c1*g) + c2*Z  (restoration_algorithms.py:232-236) */
+int psgla_langevin_update(const float* X, const float* g, float* Y, int32_t B, int64_t E, float c1,
+                          float c2, uint64_t seed, int32_t chain0, const int64_t* d_step,
+                          int64_t step_offset, void* stream);
+
+/* X = (1-alpha)*Y + alpha*D, then samples / block accumulators (restoration_algorithms.py:238-271).
+ * mean/sq are (B,C,H,W) live accumulators updated in place. */
+int psgla_relax_accumulate(const float* Y, const float* D, float* X, float alpha, int32_t alpha_is_one,
+                           float* mean, float* sq, int32_t B, int64_t E, const PsglaSchedule* s,
+                           void* stream);
+
+/* PnP-ULA update (restoration_algorithms.py:104-115) + samples / accumulators:
+ *   proj = clip(X, c_min, c_max); X' = (X + delta*((gp - (X-proj)/lambd) + gd)) + brw*Z */
+int pnpula_update(const float* X, const float* gp, const float* gd, float* Xout, float delta,
+                  float lambd, float brw, float c_min, float c_max, float* mean, float* sq,
+                  int32_t B, int64_t E, uint64_t seed, int32_t chain0, const PsglaSchedule* s,
+                  void* stream);
+
+/* g = ((-m) * (X - y)) / sigma2, mask (H,W) u8 per chain (sampling_images.py:295) */
+int psgla_inpaint_grad(const float* X, const float* y, int64_t y_chain_stride, const uint8_t* mask,
+                       int64_t mask_chain_stride, float* g, int32_t B, int32_t C, int32_t H,
+                       int32_t W, float sigma2, void* stream);
+
+/* *d_step += 1 (one thread) */
+int psgla_advance_step(int64_t* d_step, void* stream);
+
+/* Diagnostic (tests): Box-Muller radius r(k) and (cos, sin)(2 pi k 2^-24) of the noise stream for the
+ * 24-bit indices k0 .. k0+n-1, so the GPU stream can be checked against the CPU checker exhaustively. */
+int psgla_debug_bm_tables(float* r, float* cs, float* sn, uint32_t k0, uint32_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PSGLA_HIP_H_ */

@@ -91,6 +91,16 @@ def angle_table(k_begin: int, count: int):
     return c, s
 
 
+def sqrt_rn(t: torch.Tensor) -> torch.Tensor:
+    """IEEE correctly rounded fp32 square root.  The reference executes on CUDA
+    (sampling_images.py:109), where torch.sqrt(float32) is correctly rounded; torch's CPU
+    AVX-512 float sqrt is not (about 0.5 % of values differ by one ulp), so the checker takes
+    the float64 root and rounds it once to float32 -- the correctly rounded result."""
+    if t.dtype != torch.float32:
+        return torch.sqrt(t)
+    return torch.sqrt(t.double()).float()
+
+
 # --------------------------------------------------------------------------------------
 # deepinv 0.2.1 TVDenoiser (restated; see module docstring)
 # --------------------------------------------------------------------------------------
@@ -142,7 +152,7 @@ class TVDenoiser:
     @staticmethod
     def prox_sigma_g_conj(u, lambda2):
         one = torch.tensor([1], dtype=u.dtype)
-        return u / torch.maximum(torch.sqrt(torch.sum(u ** 2, axis=-1)) / lambda2, one).unsqueeze(-1)
+        return u / torch.maximum(sqrt_rn(torch.sum(u ** 2, axis=-1)) / lambda2, one).unsqueeze(-1)
 
     def forward(self, y, ths=None):
         if self.restart or self.x2 is None or self.x2.shape != y.shape:
@@ -315,7 +325,7 @@ def pnpula(init, data_grad, prior_grad, delta, lambd, n_iter=5000, n_inter=1000,
     one = torch.ones(shape, dtype=dtype)
     xmmse = torch.zeros(shape, dtype=dtype)
     xmmse2 = torch.zeros(shape, dtype=dtype)
-    brw = torch.sqrt(2 * delta)
+    brw = sqrt_rn(2 * delta)
     if seed is None:
         raise UnboundLocalError("local variable 'gen' referenced before assignment")
     if n_inter_mmse is None:

@@ -1,0 +1,884 @@
+// libpsgla_hip: MI355X (gfx950, CDNA4) kernels for the PSGLA / PnP-ULA Langevin step.
+//
+// Hot path (reference /root/reference/restoration_algorithms.py):
+//   psgla loop body   :231-271   Z ~ N(0,1); Y = X + (delta/lambd) g(X) + sqrt2 s Z;
+//                                 X = (1-alpha) Y + alpha D(Y, s); block means of X, X^2
+//   pnpula loop body  :103-144   X += delta (gp - (X - clip(X))/lambd + gd) + sqrt(2 delta) Z
+//   g(X) (inpainting) sampling_images.py:295   -mask (x - y) / sigma2
+//   D = TV prox       deepinv 0.2.1 TVDenoiser (sampling_images.py:138), warm-started
+//
+// Design: one fused kernel per Langevin step for PSGLA+TV.  A workgroup
+// of 16 waves owns a band of up to 64 rows x 256 columns of one (chain, channel)
+// plane; every lane owns 4 consecutive columns of 4 rows, so the whole TV state
+// (x2, u2) and tau*Y of the tile live in registers for all inner iterations.  The
+// inner iterations are temporally blocked: the band carries a halo of n_tv rows /
+// columns (the stencil's dependency cone grows by one pixel per iteration), which is
+// recomputed by neighbouring bands instead of being exchanged.  Horizontal
+// neighbours are lane shuffles, vertical neighbours across waves go through two
+// 16 KB LDS row buffers.  HBM traffic per element and step: read X, u2, y, mask,
+// mean, sq; write X, u2, mean, sq (44.33 B with the 1-byte mask shared by 3
+// channels); the Gaussian noise is generated in registers (Philox4x32-10).
+//
+// Floating-point: the library is compiled with -ffp-contract=off.  EXACT=true
+// kernels evaluate the reference's expressions in the reference's order with IEEE
+// division and square root and are bit-identical to the torch CPU checker
+// (oracle/); EXACT=false replaces the four TV divisions and the sqrt by
+// reciprocal/rsqrt forms and fmas (about 3x fewer VALU ops) and is checked against
+// the same checker within the north-star tolerance.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "psgla_hip.h"
+#include "noise.hpp"
+
+namespace psgla {
+
+constexpr int WAVE = 64;
+constexpr int CPL = 4;            // columns per lane
+constexpr int TV_R = 4;           // rows per wave
+constexpr int TV_NW = 16;         // waves per workgroup
+constexpr int TV_THREADS = TV_NW * WAVE;
+constexpr int TV_ROWS = TV_NW * TV_R;      // 64 rows per band (with halo)
+constexpr int TV_COLS = CPL * WAVE;        // 256 columns per segment (with halo)
+constexpr int MAXIT = PSGLA_TV_MAX_FUSED_IT;
+constexpr int MAXG = 1024;        // chains per launch (early-stop groups)
+constexpr uint32_t TAG_LANGEVIN = 0;
+
+enum Front { FRONT_INPAINT = 0, FRONT_GIVEN = 1 };
+
+struct TvArgs {
+    int B, C, H, W;
+    float* x[2];
+    float* u2[2];
+    float* x2[2];
+    float* mean[2];
+    float* sq[2];
+    const float* yin;               // FRONT_GIVEN input
+    const float* yobs;              // observation
+    long long y_cs;
+    const uint8_t* mask;
+    long long m_cs;
+    float c1, c2, sigma2, alpha;
+    float tau, opt, inv_opt, sig_tv, rho, ths, tol;
+    int n_tv;
+    unsigned long long seed;
+    int chain0;
+    int pingpong;                   // 1: buffers indexed by step parity
+    long long* d_step;
+    long long step_offset;
+    int fresh_host;
+    int* fresh_dev;
+    int per_chain_norm;
+    double* norms;
+    int* arrive;
+    int advance_step;
+    // schedule
+    int n_inter, nm;
+    const float* coef;
+    float* samples;
+    long long samples_cap;
+    float* blocks;
+    float* blocks2;
+    long long blocks_cap;
+    // tiling
+    int nbands, band_h, nsegs, seg_w, tiles, halo;
+};
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float a, float b, float c, float d) {
+    *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+}
+__device__ __forceinline__ float f4get(const float4& v, int k) {
+    return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// Block-mean accumulator + sample storage for one element (restoration_algorithms.py:240-271).
+// idx = chain*E + e within the batch; BE = B*E (slot stride of samples/blocks).
+__device__ __forceinline__ void accumulate_elem(const TvArgs& a, long long step, size_t idx, size_t BE,
+                                                float X, const float* mean_in, const float* sq_in,
+                                                float* mean_out, float* sq_out) {
+    if (a.nm >= 0 && mean_out != nullptr) {
+        const int per = a.nm + 1;
+        const int im = (int)(step % per);
+        const float ca = a.coef[2 * im], cb = a.coef[2 * im + 1];
+        float m, q;
+        if (im == 0) {
+            m = cb * X;
+            q = cb * (X * X);
+        } else {
+            m = ca * mean_in[idx] + cb * X;
+            q = ca * sq_in[idx] + cb * (X * X);
+        }
+        if (im == a.nm) {
+            const long long blk = step / per;
+            if (blk < a.blocks_cap) {
+                a.blocks[(size_t)blk * BE + idx] = m;
+                a.blocks2[(size_t)blk * BE + idx] = q;
+            }
+        } else {
+            mean_out[idx] = m;
+            sq_out[idx] = q;
+        }
+    }
+    if (a.n_inter > 0 && a.samples != nullptr && (step % a.n_inter) == 0) {
+        const long long k = step / a.n_inter;
+        if (k < a.samples_cap) a.samples[(size_t)k * BE + idx] = X;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// The fused tile: load -> Y -> n_it TV iterations in registers -> store core.
+// ---------------------------------------------------------------------------------------
+struct TvShared {
+    float ylds[TV_ROWS][TV_COLS];     // Y of the tile (prox anchor; tau*Y enters every iteration)
+    float4 zrow[TV_NW][WAVE];         // first-row z of each wave (read by the wave above)
+    float4 urow[TV_NW][WAVE];         // last-row u2[...,0] of each wave (read by the wave below)
+    float red[MAXIT][TV_NW][2];       // per-wave rel_err partial sums
+};
+
+template <bool EXACT, int FRONT, bool ALPHA1>
+__device__ __forceinline__ void tv_tile(const TvArgs& a, int plane, int tile, int n_it, bool track,
+                                        long long step, bool fresh, TvShared& sh) {
+    float4 (*zrow)[WAVE] = sh.zrow;
+    float4 (*urow)[WAVE] = sh.urow;
+    float (*red)[TV_NW][2] = sh.red;
+    constexpr int R = TV_R;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int w = threadIdx.x >> 6;
+    const int H = a.H, W = a.W, C = a.C;
+    const int b = plane / C, c = plane - b * C;
+    const int band = tile / a.nsegs, seg = tile - band * a.nsegs;
+    const int r0 = band * a.band_h, r1 = min(H, r0 + a.band_h);
+    const int e0 = max(0, r0 - a.halo), e1 = min(H, r1 + a.halo);
+    const int cc0 = seg * a.seg_w, cc1 = min(W, cc0 + a.seg_w);
+    const int f0 = max(0, cc0 - a.halo) & ~3;
+    const int gj0 = f0 + CPL * lane;
+    const size_t HW = (size_t)H * W;
+    const size_t E = (size_t)C * HW;
+    const size_t BE = (size_t)a.B * E;
+    const size_t chain_off = (size_t)b * E;
+    const size_t plane_off = chain_off + (size_t)c * HW;
+    const bool vec = (W & 3) == 0;
+
+    const int par_in = a.pingpong ? (int)(step & 1) : 0;
+    const int par_out = a.pingpong ? (int)((step + 1) & 1) : 1;
+
+    float x2[R][CPL], u0[R][CPL], u1[R][CPL], z[R][CPL];
+    int gi[R];
+    bool hasUp[R], hasDown[R];
+    bool hasLeft[CPL], hasRight[CPL], colok[CPL], colcore[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const int gj = gj0 + k;
+        colok[k] = gj < W;
+        hasLeft[k] = gj > 0;
+        hasRight[k] = gj < W - 1;
+        colcore[k] = gj >= cc0 && gj < cc1;
+    }
+
+    // ------------------------------ load + data term + noise ------------------------------
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        gi[r] = e0 + w * R + r;
+        const bool rv = gi[r] < e1;
+        hasUp[r] = gi[r] > 0;
+        hasDown[r] = gi[r] < H - 1;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            x2[r][k] = 0.f; u0[r][k] = 0.f; u1[r][k] = 0.f; z[r][k] = 0.f;
+        }
+        float4 yst = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (rv && gj0 < W) {
+            const size_t base = plane_off + (size_t)gi[r] * W + gj0;
+            float Yv[CPL], xs[CPL], us0[CPL], us1[CPL];
+            if (FRONT == FRONT_INPAINT) {
+                float X[CPL], yo[CPL], mk[CPL], Z[CPL];
+                const float* xin = a.x[par_in];
+                const float* yb = a.yobs + (size_t)b * a.y_cs + (size_t)c * HW + (size_t)gi[r] * W + gj0;
+                const uint8_t* mb = a.mask + (size_t)b * a.m_cs + (size_t)gi[r] * W + gj0;
+                if (vec) {
+                    const float4 xv = ld4(xin + base);
+                    const float4 yy = ld4(yb);
+                    const uchar4 mm = *reinterpret_cast<const uchar4*>(mb);
+                    X[0] = xv.x; X[1] = xv.y; X[2] = xv.z; X[3] = xv.w;
+                    yo[0] = yy.x; yo[1] = yy.y; yo[2] = yy.z; yo[3] = yy.w;
+                    mk[0] = (float)mm.x; mk[1] = (float)mm.y; mk[2] = (float)mm.z; mk[3] = (float)mm.w;
+                    const size_t e = ((size_t)c * H + gi[r]) * W + gj0;
+                    normal_quad(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN,
+                                (uint32_t)(e >> 2), Z);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < CPL; ++k) {
+                        const bool ok = colok[k];
+                        X[k] = ok ? xin[base + k] : 0.f;
+                        yo[k] = ok ? yb[k] : 0.f;
+                        mk[k] = ok ? (float)mb[k] : 0.f;
+                        const size_t e = ((size_t)c * H + gi[r]) * W + gj0 + k;
+                        Z[k] = ok ? normal_elem(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step,
+                                                TAG_LANGEVIN, e)
+                                  : 0.f;
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    // g = ((-m) * (x - y)) / sigma2 ; Y = (X + c1 g) + c2 Z
+                    const float g = (-mk[k] * (X[k] - yo[k])) / a.sigma2;
+                    Yv[k] = (X[k] + a.c1 * g) + a.c2 * Z[k];
+                    xs[k] = X[k];
+                }
+                if (!fresh && !ALPHA1) {
+                    const float* x2in = a.x2[par_in];
+                    if (vec) {
+                        const float4 v = ld4(x2in + base);
+                        xs[0] = v.x; xs[1] = v.y; xs[2] = v.z; xs[3] = v.w;
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < CPL; ++k) xs[k] = colok[k] ? x2in[base + k] : 0.f;
+                    }
+                }
+            } else {  // FRONT_GIVEN: standalone prox of a given tensor
+                const float* yin = a.yin;
+                const float* x2in = a.x2[0];
+                if (vec) {
+                    const float4 v = ld4(yin + base);
+                    Yv[0] = v.x; Yv[1] = v.y; Yv[2] = v.z; Yv[3] = v.w;
+                    if (!fresh) {
+                        const float4 q = ld4(x2in + base);
+                        xs[0] = q.x; xs[1] = q.y; xs[2] = q.z; xs[3] = q.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < CPL; ++k) {
+                        Yv[k] = colok[k] ? yin[base + k] : 0.f;
+                        if (!fresh) xs[k] = colok[k] ? x2in[base + k] : 0.f;
+                    }
+                }
+            }
+            if (!fresh) {
+                const float* u2in = a.u2[par_in];
+                if (vec) {
+                    const float4 p = ld4(u2in + 2 * base);
+                    const float4 q = ld4(u2in + 2 * base + 4);
+                    us0[0] = p.x; us1[0] = p.y; us0[1] = p.z; us1[1] = p.w;
+                    us0[2] = q.x; us1[2] = q.y; us0[3] = q.z; us1[3] = q.w;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < CPL; ++k) {
+                        us0[k] = colok[k] ? u2in[2 * (base + k)] : 0.f;
+                        us1[k] = colok[k] ? u2in[2 * (base + k) + 1] : 0.f;
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                if (!colok[k]) continue;
+                x2[r][k] = fresh ? Yv[k] : xs[k];
+                u0[r][k] = fresh ? 0.f : us0[k];
+                u1[r][k] = fresh ? 0.f : us1[k];
+            }
+            yst = make_float4(colok[0] ? Yv[0] : 0.f, colok[1] ? Yv[1] : 0.f, colok[2] ? Yv[2] : 0.f,
+                              colok[3] ? Yv[3] : 0.f);
+        }
+        *reinterpret_cast<float4*>(&sh.ylds[w * R + r][CPL * lane]) = yst;
+    }
+
+    urow[w][lane] = make_float4(u0[R - 1][0], u0[R - 1][1], u0[R - 1][2], u0[R - 1][3]);
+    __syncthreads();
+
+    // ------------------------------ inner TV iterations ------------------------------
+    for (int it = 0; it < n_it; ++it) {
+        const bool trk = track && it >= 2 && it <= a.n_tv - 2;
+        float sd = 0.f, sn = 0.f;
+        // Phase A: x = prox_tau_fx(x2 - tau nabla^T u2, y); z = 2x - x2; x2 += rho (x - x2)
+        const float4 up = (w > 0) ? urow[w - 1][lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const float u1l = __shfl_up(u1[r][CPL - 1], 1);
+            const float4 yrow = *reinterpret_cast<const float4*>(&sh.ylds[w * R + r][CPL * lane]);
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const float u0up = (r > 0) ? u0[r - 1][k] : f4get(up, k);
+                const float u1left = (k > 0) ? u1[r][k - 1] : u1l;
+                // nabla_adjoint in deepinv's order: ((0 - u0) + u0[i-1]) - u1) + u1[j-1]
+                float t = hasDown[r] ? (0.0f - u0[r][k]) : 0.0f;
+                t = hasUp[r] ? t + u0up : t;
+                t = hasRight[k] ? t - u1[r][k] : t;
+                t = hasLeft[k] ? t + u1left : t;
+                const float xo = x2[r][k];
+                float xv, zv, xn;
+                if (EXACT) {
+                    xv = ((xo - a.tau * t) + a.tau * f4get(yrow, k)) / a.opt;
+                    zv = 2.0f * xv - xo;
+                    xn = xo + a.rho * (xv - xo);
+                } else {
+                    xv = __builtin_fmaf(a.tau, f4get(yrow, k) - t, xo) * a.inv_opt;
+                    zv = __builtin_fmaf(2.0f, xv, -xo);
+                    xn = __builtin_fmaf(a.rho, xv - xo, xo);
+                }
+                if (trk) {
+                    const bool core = colcore[k] && gi[r] >= r0 && gi[r] < r1;
+                    const float d = xo - xn;
+                    const float q = xn + 1e-12f;
+                    sd += core ? d * d : 0.f;
+                    sn += core ? q * q : 0.f;
+                }
+                z[r][k] = zv;
+                x2[r][k] = xn;
+            }
+        }
+        zrow[w][lane] = make_float4(z[0][0], z[0][1], z[0][2], z[0][3]);
+        if (trk) {
+            sd = wave_sum(sd);
+            sn = wave_sum(sn);
+            if (lane == 0) { red[it][w][0] = sd; red[it][w][1] = sn; }
+        }
+        __syncthreads();
+        // Phase B: u = prox_sigma_g_conj(u2 + sigma nabla z, ths); u2 += rho (u - u2)
+        const float4 dn = (w < TV_NW - 1) ? zrow[w + 1][lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const float zr3 = __shfl_down(z[r][0], 1);
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const float zc = z[r][k];
+                const float zd = (r < R - 1) ? z[r + 1][k] : f4get(dn, k);
+                const float zr = (k < CPL - 1) ? z[r][k + 1] : zr3;
+                const float g0 = hasDown[r] ? ((0.0f - zc) + zd) : 0.0f;
+                const float g1 = hasRight[k] ? ((0.0f - zc) + zr) : 0.0f;
+                const float uo0 = u0[r][k], uo1 = u1[r][k];
+                if (EXACT) {
+                    const float v0 = uo0 + a.sig_tv * g0;
+                    const float v1 = uo1 + a.sig_tv * g1;
+                    const float nrm = sqrtf(v0 * v0 + v1 * v1) / a.ths;
+                    const float dd = fmaxf(nrm, 1.0f);
+                    const float n0 = v0 / dd, n1 = v1 / dd;
+                    u0[r][k] = uo0 + a.rho * (n0 - uo0);
+                    u1[r][k] = uo1 + a.rho * (n1 - uo1);
+                } else {
+                    const float v0 = __builtin_fmaf(a.sig_tv, g0, uo0);
+                    const float v1 = __builtin_fmaf(a.sig_tv, g1, uo1);
+                    const float s2 = __builtin_fmaf(v0, v0, v1 * v1);
+                    const float f = fminf(1.0f, a.ths * __builtin_amdgcn_rsqf(s2));
+                    u0[r][k] = __builtin_fmaf(a.rho, __builtin_fmaf(v0, f, -uo0), uo0);
+                    u1[r][k] = __builtin_fmaf(a.rho, __builtin_fmaf(v1, f, -uo1), uo1);
+                }
+            }
+        }
+        urow[w][lane] = make_float4(u0[R - 1][0], u0[R - 1][1], u0[R - 1][2], u0[R - 1][3]);
+        __syncthreads();
+    }
+
+    // rel_err partial sums -> global (one fp64 atomic per iteration and workgroup)
+    if (track && n_it >= 4) {
+        const int t = threadIdx.x;
+        if (t >= 2 && t <= a.n_tv - 2) {
+            double sd = 0.0, sn = 0.0;
+            for (int ww = 0; ww < TV_NW; ++ww) { sd += red[t][ww][0]; sn += red[t][ww][1]; }
+            const int g = a.per_chain_norm ? b : 0;
+            atomicAdd(&a.norms[((size_t)g * a.n_tv + t) * 2], sd);
+            atomicAdd(&a.norms[((size_t)g * a.n_tv + t) * 2 + 1], sn);
+        }
+    }
+
+    // ------------------------------ store the core ------------------------------
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (gi[r] < r0 || gi[r] >= r1) continue;
+        const size_t base = plane_off + (size_t)gi[r] * W + gj0;
+        float Xo[CPL];
+        const float4 yrow = *reinterpret_cast<const float4*>(&sh.ylds[w * R + r][CPL * lane]);
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            // X = (1 - alpha) Y + alpha D(Y)  (restoration_algorithms.py:238); alpha == 1 gives D(Y) exactly
+            if (FRONT == FRONT_INPAINT && !ALPHA1)
+                Xo[k] = (1.0f - a.alpha) * f4get(yrow, k) + a.alpha * x2[r][k];
+            else
+                Xo[k] = x2[r][k];
+        }
+        float* xout = (FRONT == FRONT_INPAINT) ? a.x[par_out] : a.x2[1];
+        float* u2out = a.u2[par_out];
+        if (vec && colcore[0]) {
+            st4(xout + base, Xo[0], Xo[1], Xo[2], Xo[3]);
+            st4(u2out + 2 * base, u0[r][0], u1[r][0], u0[r][1], u1[r][1]);
+            st4(u2out + 2 * base + 4, u0[r][2], u1[r][2], u0[r][3], u1[r][3]);
+            if (FRONT == FRONT_INPAINT && !ALPHA1)
+                st4(a.x2[par_out] + base, x2[r][0], x2[r][1], x2[r][2], x2[r][3]);
+        } else if (!vec) {
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                if (!colcore[k]) continue;
+                xout[base + k] = Xo[k];
+                u2out[2 * (base + k)] = u0[r][k];
+                u2out[2 * (base + k) + 1] = u1[r][k];
+                if (FRONT == FRONT_INPAINT && !ALPHA1) a.x2[par_out][base + k] = x2[r][k];
+            }
+        }
+        if (FRONT == FRONT_INPAINT) {
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                if (!colcore[k]) continue;
+                const size_t idx = base + k;   // == chain*E + e
+                accumulate_elem(a, step, idx, BE, Xo[k], a.mean[par_in], a.sq[par_in], a.mean[par_out],
+                                a.sq[par_out]);
+            }
+        }
+    }
+    (void)chain_off;
+}
+
+template <bool EXACT, int FRONT, bool ALPHA1>
+__global__ void __launch_bounds__(TV_THREADS) tv_main_kernel(const TvArgs a) {
+    __shared__ TvShared sh;
+    const long long step = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
+    const bool fresh = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
+    const int P = a.B * a.C;
+    const int T = a.tiles;
+    // XCD-aware order: blocks x and x+8 share an XCD (round-robin dispatch), so all
+    // tiles of one plane land on one XCD and their halo rows hit that XCD's L2.
+    const int x = blockIdx.x;
+    const int xcd = x & 7;
+    const int k = x >> 3;
+    const int plane = (k / T) * 8 + xcd;
+    const int tile = k - (k / T) * T;
+    if (plane >= P) return;
+    tv_tile<EXACT, FRONT, ALPHA1>(a, plane, tile, a.n_tv, true, step, fresh, sh);
+}
+
+// Early-stop finaliser (deepinv: break when rel_err < tol at inner iteration >= 2): recompute
+// the tiles of the affected chains with the right number of inner iterations, then reset the
+// workspace, clear the restart flag and advance the step counter (last block to arrive).
+template <bool EXACT, int FRONT, bool ALPHA1>
+__global__ void __launch_bounds__(TV_THREADS) tv_finalise_kernel(const TvArgs a) {
+    __shared__ TvShared sh;
+    __shared__ int s_stop[MAXG];
+    __shared__ int s_flag;
+    const long long step = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
+    const bool fresh = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
+    const int P = a.B * a.C;
+    const int T = a.tiles;
+    const int G = a.per_chain_norm ? a.B : 1;
+    if (threadIdx.x == 0) s_flag = 0;
+    __syncthreads();
+    for (int g = threadIdx.x; g < G; g += blockDim.x) {
+        int stop = a.n_tv;
+        for (int t = 2; t <= a.n_tv - 2; ++t) {
+            const double nd = a.norms[((size_t)g * a.n_tv + t) * 2];
+            const double nn = a.norms[((size_t)g * a.n_tv + t) * 2 + 1];
+            const float rel = (float)sqrt(nd) / (float)sqrt(nn);
+            if (rel < a.tol) { stop = t + 1; break; }
+        }
+        s_stop[g] = stop;
+        if (stop < a.n_tv) atomicOr(&s_flag, 1);
+    }
+    __syncthreads();
+    if (s_flag) {
+        for (int item = blockIdx.x; item < P * T; item += gridDim.x) {
+            const int plane = item / T, tile = item - (item / T) * T;
+            const int g = a.per_chain_norm ? plane / a.C : 0;
+            if (s_stop[g] < a.n_tv) tv_tile<EXACT, FRONT, ALPHA1>(a, plane, tile, s_stop[g], false, step, fresh, sh);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const int old = atomicAdd(a.arrive, 1);
+        s_flag = (old == (int)gridDim.x - 1) ? 2 : 0;
+    }
+    __syncthreads();
+    if (s_flag == 2) {
+        __threadfence();
+        const int n = G * a.n_tv * 2;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) a.norms[i] = 0.0;
+        if (threadIdx.x == 0) {
+            *a.arrive = 0;
+            if (a.fresh_dev) *a.fresh_dev = 0;
+            if (a.advance_step && a.d_step) *a.d_step = *a.d_step + 1;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Generic elementwise kernels (opaque closures; also the first / last steps of fused paths)
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ long long read_step(const long long* d, long long off) {
+    return (d ? *d : 0LL) + off;
+}
+
+__global__ void normal_fill_kernel(float* out, int B, long long E, unsigned long long seed, int chain0,
+                                   const long long* d_step, long long off, uint32_t tag) {
+    const long long step = read_step(d_step, off);
+    const long long Q = (E + 3) >> 2;
+    const long long total = (long long)B * Q;
+    for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int b = (int)(t / Q);
+        const long long q = t - (long long)b * Q;
+        float z[4];
+        normal_quad(seed, (uint32_t)(chain0 + b), (uint32_t)step, tag, (uint32_t)q, z);
+        const long long e = q << 2;
+        float* o = out + (size_t)b * E + e;
+        if (e + 3 < E && ((E & 3) == 0)) {
+            *reinterpret_cast<float4*>(o) = make_float4(z[0], z[1], z[2], z[3]);
+        } else {
+            for (int j = 0; j < 4; ++j)
+                if (e + j < E) o[j] = z[j];
+        }
+    }
+}
+
+// Y = (X + c1 g) + c2 Z   (restoration_algorithms.py:236)
+__global__ void langevin_update_kernel(const float* X, const float* g, float* Y, int B, long long E,
+                                       float c1, float c2, unsigned long long seed, int chain0,
+                                       const long long* d_step, long long off) {
+    const long long step = read_step(d_step, off);
+    const long long Q = (E + 3) >> 2;
+    const long long total = (long long)B * Q;
+    for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int b = (int)(t / Q);
+        const long long q = t - (long long)b * Q;
+        float z[4];
+        normal_quad(seed, (uint32_t)(chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)q, z);
+        const size_t i0 = (size_t)b * E + (size_t)(q << 2);
+        for (int j = 0; j < 4; ++j) {
+            if ((q << 2) + j < E) Y[i0 + j] = (X[i0 + j] + c1 * g[i0 + j]) + c2 * z[j];
+        }
+    }
+}
+
+struct AccArgs {
+    int n_inter, nm;
+    const float* coef;
+    float* samples;
+    long long samples_cap;
+    float* blocks;
+    float* blocks2;
+    long long blocks_cap;
+    const long long* d_step;
+    long long off;
+};
+
+__device__ __forceinline__ void acc_elem(const AccArgs& s, long long step, size_t idx, size_t BE, float X,
+                                         float* mean, float* sq) {
+    if (s.nm >= 0 && mean != nullptr) {
+        const int per = s.nm + 1;
+        const int im = (int)(step % per);
+        const float ca = s.coef[2 * im], cb = s.coef[2 * im + 1];
+        float m, q;
+        if (im == 0) {
+            m = cb * X;
+            q = cb * (X * X);
+        } else {
+            m = ca * mean[idx] + cb * X;
+            q = ca * sq[idx] + cb * (X * X);
+        }
+        if (im == s.nm) {
+            const long long blk = step / per;
+            if (blk < s.blocks_cap) {
+                s.blocks[(size_t)blk * BE + idx] = m;
+                s.blocks2[(size_t)blk * BE + idx] = q;
+            }
+        } else {
+            mean[idx] = m;
+            sq[idx] = q;
+        }
+    }
+    if (s.n_inter > 0 && s.samples != nullptr && (step % s.n_inter) == 0) {
+        const long long k = step / s.n_inter;
+        if (k < s.samples_cap) s.samples[(size_t)k * BE + idx] = X;
+    }
+}
+
+// X = (1 - alpha) Y + alpha D ; accumulate   (restoration_algorithms.py:238-271)
+__global__ void relax_accumulate_kernel(const float* Y, const float* D, float* X, float alpha,
+                                        int B, long long E, float* mean, float* sq, AccArgs s) {
+    const long long step = read_step(s.d_step, s.off);
+    const size_t BE = (size_t)B * E;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < BE;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const float x = (1.0f - alpha) * Y[i] + alpha * D[i];
+        X[i] = x;
+        acc_elem(s, step, i, BE, x, mean, sq);
+    }
+}
+
+// PnP-ULA (restoration_algorithms.py:104-115)
+__global__ void pnpula_update_kernel(const float* X, const float* gp, const float* gd, float* Xo,
+                                     float delta, float lambd, float brw, float cmin, float cmax, int B,
+                                     long long E, float* mean, float* sq, unsigned long long seed,
+                                     int chain0, AccArgs s) {
+    const long long step = read_step(s.d_step, s.off);
+    const long long Q = (E + 3) >> 2;
+    const long long total = (long long)B * Q;
+    const size_t BE = (size_t)B * E;
+    for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int b = (int)(t / Q);
+        const long long q = t - (long long)b * Q;
+        float z[4];
+        normal_quad(seed, (uint32_t)(chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)q, z);
+        const size_t i0 = (size_t)b * E + (size_t)(q << 2);
+        for (int j = 0; j < 4; ++j) {
+            if ((q << 2) + j >= E) break;
+            const size_t i = i0 + j;
+            const float x = X[i];
+            const float out = (x > cmin) ? x : cmin;
+            const float proj = (out < cmax) ? out : cmax;
+            const float gpi = (gp[i] - (x - proj) / lambd) + gd[i];
+            const float xn = (x + delta * gpi) + brw * z[j];
+            Xo[i] = xn;
+            acc_elem(s, step, i, BE, xn, mean, sq);
+        }
+    }
+}
+
+// g = ((-m) (X - y)) / sigma2   (sampling_images.py:295)
+__global__ void inpaint_grad_kernel(const float* X, const float* y, long long y_cs, const uint8_t* mask,
+                                    long long m_cs, float* g, int B, int C, int H, int W, float sigma2) {
+    const size_t HW = (size_t)H * W, E = (size_t)C * HW, BE = (size_t)B * E;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < BE;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const size_t b = i / E, e = i - b * E;
+        const size_t p = e % HW;
+        const float m = (float)mask[b * m_cs + p];
+        g[i] = (-m * (X[i] - y[b * y_cs + e])) / sigma2;
+    }
+}
+
+__global__ void advance_step_kernel(long long* d) { *d = *d + 1; }
+
+// Diagnostic: the Box-Muller radius / angle for 24-bit indices [k0, k0+n) (exhaustive noise test).
+__global__ void bm_tables_kernel(float* r, float* cs, float* sn, uint32_t k0, uint32_t n) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t k = k0 + i;
+        r[i] = bm_radius(k);
+        float c, s;
+        bm_angle(k, c, s);
+        cs[i] = c;
+        sn[i] = s;
+    }
+}
+
+}  // namespace psgla
+
+// =======================================================================================
+// C ABI
+// =======================================================================================
+using namespace psgla;
+
+static thread_local char g_err[512] = "";
+
+static int fail(int code, const char* msg) {
+    snprintf(g_err, sizeof(g_err), "%s", msg);
+    return code ? code : (int)hipErrorInvalidValue;
+}
+
+static int launch_check(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+        return (int)e;
+    }
+    return 0;
+}
+
+static int grid_for(long long n, int threads) {
+    long long g = (n + threads - 1) / threads;
+    if (g > 256 * 16) g = 256 * 16;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+static void tv_tiling(TvArgs& a) {
+    const int h = a.halo;
+    if (a.H <= TV_ROWS) {
+        a.band_h = a.H; a.nbands = 1;
+    } else {
+        const int bh = TV_ROWS - 2 * h;
+        a.nbands = (a.H + bh - 1) / bh;
+        a.band_h = (a.H + a.nbands - 1) / a.nbands;
+    }
+    if (a.W <= TV_COLS) {
+        a.seg_w = a.W; a.nsegs = 1;
+    } else {
+        const int sw = (TV_COLS - 2 * h - 3) & ~3;
+        a.nsegs = (a.W + sw - 1) / sw;
+        a.seg_w = (((a.W + a.nsegs - 1) / a.nsegs) + 3) & ~3;
+    }
+    a.tiles = a.nbands * a.nsegs;
+}
+
+template <bool EXACT, int FRONT, bool ALPHA1>
+static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
+    const int P = a.B * a.C;
+    if (mask == 0) mask = 3;
+    if (mask & 1) {
+        const int grid_main = ((P + 7) / 8) * 8 * a.tiles;
+        hipLaunchKernelGGL((tv_main_kernel<EXACT, FRONT, ALPHA1>), dim3(grid_main), dim3(TV_THREADS), 0, st, a);
+        int rc = launch_check("tv_kernel(main)");
+        if (rc) return rc;
+    }
+    if (!(mask & 2)) return 0;
+    const int grid_fin = (P * a.tiles < 256) ? P * a.tiles : 256;
+    hipLaunchKernelGGL((tv_finalise_kernel<EXACT, FRONT, ALPHA1>), dim3(grid_fin), dim3(TV_THREADS), 0, st, a);
+    return launch_check("tv_kernel(finalise)");
+}
+
+static int check_tv_common(int B, int C, int H, int W, int n_tv) {
+    if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return fail(0, "psgla: empty tensor dimensions");
+    if (B > MAXG) return fail(0, "psgla: more than 1024 chains in one launch; split the batch");
+    if (n_tv < 0 || n_tv > MAXIT)
+        return fail(0, "psgla: n_it_max outside [0, PSGLA_TV_MAX_FUSED_IT] for the fused TV kernel");
+    if (H > TV_ROWS && TV_ROWS - 2 * n_tv < 1) return fail(0, "psgla: TV halo too large");
+    return 0;
+}
+
+extern "C" {
+
+int psgla_abi_version(void) { return PSGLA_HIP_ABI_VERSION; }
+const char* psgla_last_error(void) { return g_err; }
+
+int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream) {
+    if (!d || !s) return fail(0, "psgla_tv_step: null descriptor");
+    int rc = check_tv_common(d->B, d->C, d->H, d->W, d->n_tv);
+    if (rc) return rc;
+    const bool alpha1 = d->x2[0] == nullptr;
+    if (!d->x[0] || !d->x[1] || !d->u2[0] || !d->u2[1] || !d->y || !d->mask || !d->norms || !d->arrive ||
+        !d->fresh)
+        return fail(0, "psgla_tv_step: missing buffer");
+    if (!alpha1 && !d->x2[1]) return fail(0, "psgla_tv_step: x2[1] missing");
+    if (s->n_inter_mmse >= 0 && (!d->mean[0] || !d->mean[1] || !d->sq[0] || !d->sq[1] || !s->acc_coef))
+        return fail(0, "psgla_tv_step: accumulators missing");
+    TvArgs a;
+    memset(&a, 0, sizeof(a));
+    a.B = d->B; a.C = d->C; a.H = d->H; a.W = d->W;
+    for (int i = 0; i < 2; ++i) {
+        a.x[i] = d->x[i]; a.u2[i] = d->u2[i]; a.x2[i] = d->x2[i]; a.mean[i] = d->mean[i]; a.sq[i] = d->sq[i];
+    }
+    a.yobs = d->y; a.y_cs = d->y_chain_stride; a.mask = d->mask; a.m_cs = d->mask_chain_stride;
+    a.c1 = d->c1; a.c2 = d->c2; a.sigma2 = d->sigma2; a.alpha = d->alpha;
+    a.tau = d->tau; a.opt = d->one_plus_tau; a.inv_opt = (float)(1.0 / (double)d->one_plus_tau);
+    a.sig_tv = d->sigma_tv; a.rho = d->rho; a.ths = d->ths; a.tol = d->tol;
+    a.n_tv = d->n_tv; a.seed = d->seed; a.chain0 = d->chain0; a.pingpong = 1;
+    a.d_step = (long long*)s->d_step; a.step_offset = s->step_offset;
+    a.fresh_dev = d->fresh; a.per_chain_norm = 1; a.norms = d->norms; a.arrive = d->arrive;
+    a.advance_step = d->advance_step;
+    a.n_inter = s->n_inter; a.nm = s->n_inter_mmse; a.coef = s->acc_coef;
+    a.samples = s->samples; a.samples_cap = s->samples_cap;
+    a.blocks = s->blocks; a.blocks2 = s->blocks2; a.blocks_cap = s->blocks_cap;
+    a.halo = d->n_tv;
+    tv_tiling(a);
+    hipStream_t st = (hipStream_t)stream;
+    const int m = d->launch_mask;
+    if (d->exact)
+        return alpha1 ? launch_tv<true, FRONT_INPAINT, true>(a, st, m) : launch_tv<true, FRONT_INPAINT, false>(a, st, m);
+    return alpha1 ? launch_tv<false, FRONT_INPAINT, true>(a, st, m) : launch_tv<false, FRONT_INPAINT, false>(a, st, m);
+}
+
+int psgla_tv_prox(const PsglaTvProx* d, void* stream) {
+    if (!d) return fail(0, "psgla_tv_prox: null descriptor");
+    int rc = check_tv_common(d->B, d->C, d->H, d->W, d->n_tv);
+    if (rc) return rc;
+    if (!d->y || !d->x2_out || !d->u2_out || !d->norms || !d->arrive) return fail(0, "psgla_tv_prox: missing buffer");
+    if (!d->fresh && (!d->x2_in || !d->u2_in)) return fail(0, "psgla_tv_prox: warm start needs x2_in/u2_in");
+    TvArgs a;
+    memset(&a, 0, sizeof(a));
+    a.B = d->B; a.C = d->C; a.H = d->H; a.W = d->W;
+    a.yin = d->y;
+    a.x2[0] = const_cast<float*>(d->x2_in); a.x2[1] = d->x2_out;
+    a.u2[0] = const_cast<float*>(d->u2_in); a.u2[1] = d->u2_out;
+    a.tau = d->tau; a.opt = d->one_plus_tau; a.inv_opt = (float)(1.0 / (double)d->one_plus_tau);
+    a.sig_tv = d->sigma_tv; a.rho = d->rho; a.ths = d->ths; a.tol = d->tol;
+    a.n_tv = d->n_tv; a.pingpong = 0;
+    a.fresh_host = d->fresh; a.per_chain_norm = 0; a.norms = d->norms; a.arrive = d->arrive;
+    a.nm = -1;
+    a.halo = d->n_tv;
+    tv_tiling(a);
+    hipStream_t st = (hipStream_t)stream;
+    return d->exact ? launch_tv<true, FRONT_GIVEN, true>(a, st) : launch_tv<false, FRONT_GIVEN, true>(a, st);
+}
+
+int psgla_normal_fill(float* out, int32_t B, int64_t E, uint64_t seed, int32_t chain0, const int64_t* d_step,
+                      int64_t step_offset, uint32_t tag, void* stream) {
+    if (!out || B <= 0 || E <= 0) return fail(0, "psgla_normal_fill: bad arguments");
+    const long long total = (long long)B * ((E + 3) / 4);
+    hipLaunchKernelGGL(normal_fill_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, out, B,
+                       (long long)E, (unsigned long long)seed, chain0, (const long long*)d_step,
+                       (long long)step_offset, tag);
+    return launch_check("normal_fill");
+}
+
+int psgla_langevin_update(const float* X, const float* g, float* Y, int32_t B, int64_t E, float c1, float c2,
+                          uint64_t seed, int32_t chain0, const int64_t* d_step, int64_t step_offset,
+                          void* stream) {
+    if (!X || !g || !Y || B <= 0 || E <= 0) return fail(0, "psgla_langevin_update: bad arguments");
+    const long long total = (long long)B * ((E + 3) / 4);
+    hipLaunchKernelGGL(langevin_update_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, X,
+                       g, Y, B, (long long)E, c1, c2, (unsigned long long)seed, chain0,
+                       (const long long*)d_step, (long long)step_offset);
+    return launch_check("langevin_update");
+}
+
+static AccArgs make_acc(const PsglaSchedule* s) {
+    AccArgs a;
+    a.n_inter = s->n_inter; a.nm = s->n_inter_mmse; a.coef = s->acc_coef;
+    a.samples = s->samples; a.samples_cap = s->samples_cap;
+    a.blocks = s->blocks; a.blocks2 = s->blocks2; a.blocks_cap = s->blocks_cap;
+    a.d_step = (const long long*)s->d_step; a.off = s->step_offset;
+    return a;
+}
+
+int psgla_relax_accumulate(const float* Y, const float* D, float* X, float alpha, int32_t alpha_is_one,
+                           float* mean, float* sq, int32_t B, int64_t E, const PsglaSchedule* s, void* stream) {
+    (void)alpha_is_one;
+    if (!Y || !D || !X || !s || B <= 0 || E <= 0) return fail(0, "psgla_relax_accumulate: bad arguments");
+    if (s->n_inter_mmse >= 0 && (!mean || !sq || !s->acc_coef)) return fail(0, "psgla_relax_accumulate: accumulators missing");
+    const long long total = (long long)B * E;
+    hipLaunchKernelGGL(relax_accumulate_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, Y,
+                       D, X, alpha, B, (long long)E, mean, sq, make_acc(s));
+    return launch_check("relax_accumulate");
+}
+
+int pnpula_update(const float* X, const float* gp, const float* gd, float* Xout, float delta, float lambd,
+                  float brw, float c_min, float c_max, float* mean, float* sq, int32_t B, int64_t E,
+                  uint64_t seed, int32_t chain0, const PsglaSchedule* s, void* stream) {
+    if (!X || !gp || !gd || !Xout || !s || B <= 0 || E <= 0) return fail(0, "pnpula_update: bad arguments");
+    if (s->n_inter_mmse >= 0 && (!mean || !sq || !s->acc_coef)) return fail(0, "pnpula_update: accumulators missing");
+    const long long total = (long long)B * ((E + 3) / 4);
+    hipLaunchKernelGGL(pnpula_update_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, X, gp,
+                       gd, Xout, delta, lambd, brw, c_min, c_max, B, (long long)E, mean, sq,
+                       (unsigned long long)seed, chain0, make_acc(s));
+    return launch_check("pnpula_update");
+}
+
+int psgla_inpaint_grad(const float* X, const float* y, int64_t y_chain_stride, const uint8_t* mask,
+                       int64_t mask_chain_stride, float* g, int32_t B, int32_t C, int32_t H, int32_t W, float sigma2,
+                       void* stream) {
+    if (!X || !y || !mask || !g || B <= 0 || C <= 0 || H <= 0 || W <= 0) return fail(0, "psgla_inpaint_grad: bad arguments");
+    const long long total = (long long)B * C * H * W;
+    hipLaunchKernelGGL(inpaint_grad_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, X, y,
+                       (long long)y_chain_stride, mask, (long long)mask_chain_stride, g, B, C, H, W, sigma2);
+    return launch_check("inpaint_grad");
+}
+
+int psgla_debug_bm_tables(float* r, float* cs, float* sn, uint32_t k0, uint32_t n, void* stream) {
+    if (!r || !cs || !sn) return fail(0, "psgla_debug_bm_tables: null");
+    hipLaunchKernelGGL(bm_tables_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, r, cs, sn, k0, n);
+    return launch_check("bm_tables");
+}
+
+int psgla_advance_step(int64_t* d_step, void* stream) {
+    if (!d_step) return fail(0, "psgla_advance_step: null");
+    hipLaunchKernelGGL(advance_step_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, (long long*)d_step);
+    return launch_check("advance_step");
+}
+
+}  // extern "C"

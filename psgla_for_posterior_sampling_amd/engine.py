@@ -1,0 +1,176 @@
+"""Batched, graph-replayable PSGLA engines over the fused HIP steps.
+
+``FusedTvChains`` runs B independent PSGLA chains (inpainting fidelity + warm-started TV
+prox) with one fused kernel launch (+ one small finaliser) per Langevin step:
+restoration_algorithms.py:231-271 with the closures of sampling_images.py:295 and the
+deepinv TVDenoiser of sampling_images.py:138.  All step-dependent quantities (noise
+counter, block coefficients, sample / block slots, ping-pong parity) are derived on the
+device from a step counter, so any number of steps can be captured once in a hipGraph
+(``torch.cuda.CUDAGraph``) and replayed.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native as N
+from . import hip_ops as K
+
+
+class FusedTvChains:
+    def __init__(self, init: torch.Tensor, y: torch.Tensor, mask_u8: torch.Tensor, *, c1: float, c2: float,
+                 sigma2: float, alpha: float, ths: float, tv: K.TvConstants, seed: int, n_iter: int,
+                 n_inter: int, n_inter_mmse: int, chain0: int = 0, exact: bool = False,
+                 tv_x2: torch.Tensor | None = None, tv_u2: torch.Tensor | None = None,
+                 store_samples: bool = True, store_blocks: bool = True):
+        if init.dim() != 4:
+            raise ValueError("init must be (B, C, H, W)")
+        if tv.n_it > N.TV_MAX_FUSED_IT:
+            raise ValueError(f"fused TV step supports n_it_max <= {N.TV_MAX_FUSED_IT}")
+        dev = init.device
+        B, C, H, Wd = init.shape
+        self.shape = (B, C, H, Wd)
+        self.device = dev
+        self.alpha = float(alpha)
+        self.alpha1 = self.alpha == 1.0
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.x = [init.contiguous().clone(), torch.empty(self.shape, **f32)]
+        self.u2 = [torch.zeros(self.shape + (2,), **f32), torch.empty(self.shape + (2,), **f32)]
+        self.mean = [torch.zeros(self.shape, **f32), torch.zeros(self.shape, **f32)]
+        self.sq = [torch.zeros(self.shape, **f32), torch.zeros(self.shape, **f32)]
+        self.x2 = None
+        warm = tv_x2 is not None and tuple(tv_x2.shape) == self.shape
+        if not self.alpha1 or warm:
+            self.x2 = [torch.empty(self.shape, **f32), torch.empty(self.shape, **f32)]
+        if warm:
+            self.x2[0].copy_(tv_x2)
+            self.u2[0].copy_(tv_u2)
+        self.y = y.contiguous()
+        self.mask = mask_u8.contiguous()
+        self.sched = K.Schedule(self.shape, n_iter, n_inter, n_inter_mmse, dev, store_samples, store_blocks)
+        self.work = K.TvWorkspace(B, tv.n_it, dev)
+        self.work.fresh.fill_(0 if warm else 1)
+        self.steps_done = 0
+        self.n_iter = int(n_iter)
+        self.warm_first = warm and self.alpha1
+
+        d = N.PsglaTvStep()
+        d.B, d.C, d.H, d.W = B, C, H, Wd
+        for i in range(2):
+            d.x[i] = self.x[i].data_ptr()
+            d.u2[i] = self.u2[i].data_ptr()
+            d.mean[i] = self.mean[i].data_ptr()
+            d.sq[i] = self.sq[i].data_ptr()
+            d.x2[i] = self.x2[i].data_ptr() if (self.x2 is not None and not self.alpha1) else None
+        d.y = K._ptr(self.y, name="y")
+        d.y_chain_stride = 0 if self.y.shape[0] == 1 else C * H * Wd
+        d.mask = K._ptr(self.mask, torch.uint8, "mask")
+        d.mask_chain_stride = 0 if (self.mask.dim() == 2 or self.mask.shape[0] == 1) else H * Wd
+        d.c1, d.c2, d.sigma2, d.alpha = c1, c2, sigma2, self.alpha
+        d.tau, d.one_plus_tau, d.sigma_tv, d.rho = tv.tau, tv.one_plus_tau, tv.sigma_tv, tv.rho
+        d.ths = float(np.float32(ths))
+        d.tol = tv.tol
+        d.n_tv = tv.n_it
+        d.exact = int(bool(exact))
+        d.seed = int(seed) & (2 ** 64 - 1)
+        d.chain0 = int(chain0)
+        d.advance_step = 1
+        d.fresh = self.work.fresh.data_ptr()
+        d.norms = self.work.norms.data_ptr()
+        d.arrive = self.work.arrive.data_ptr()
+        self.desc = d
+        self.sched_struct = self.sched.struct(True, 0)
+        if self.warm_first:
+            # first step of a warm-started run: the TV primal x2 (previous run's state) is not X
+            d0 = N.PsglaTvStep.from_buffer_copy(d)
+            d0.x2[0] = self.x2[0].data_ptr()
+            d0.x2[1] = self.x2[1].data_ptr()
+            self.desc_first = d0
+        self.graph = None
+        self.graph_steps = 0
+
+    # -- stepping -----------------------------------------------------------------
+    def _launch(self, desc):
+        N.check(N.lib().psgla_tv_step(ctypes.byref(desc), ctypes.byref(self.sched_struct), K._stream()),
+                "psgla_tv_step")
+
+    def step(self, n: int = 1):
+        """Launch n steps eagerly (async on the current stream)."""
+        for _ in range(n):
+            if self.steps_done >= self.n_iter:
+                raise RuntimeError("all n_iter steps already done")
+            if self.steps_done == 0 and self.warm_first:
+                self._launch(self.desc_first)
+            else:
+                self._launch(self.desc)
+            self.steps_done += 1
+
+    def capture(self, steps_per_graph: int):
+        """Capture `steps_per_graph` identical steps into one hipGraph (after step 0)."""
+        if self.steps_done == 0 and self.warm_first:
+            self.step(1)
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(steps_per_graph):
+                self._launch(self.desc)
+        torch.cuda.current_stream().wait_stream(s)
+        self.graph = g
+        self.graph_steps = steps_per_graph
+
+    def replay(self, times: int = 1):
+        for _ in range(times):
+            if self.steps_done + self.graph_steps > self.n_iter:
+                raise RuntimeError("replay would exceed n_iter")
+            self.graph.replay()
+            self.steps_done += self.graph_steps
+
+    def launch_main_only(self, n: int = 1):
+        """Launch only the fused tile kernel n times for the CURRENT step (idempotent: it reads
+        the step's inputs and rewrites the same outputs; the step counter does not move).
+        Used to time the dominant kernel alone."""
+        d = N.PsglaTvStep.from_buffer_copy(self.desc)
+        d.launch_mask = 1
+        for _ in range(n):
+            self._launch(d)
+
+    def run(self, n: int | None = None, graph_steps: int = 0):
+        n = self.n_iter - self.steps_done if n is None else n
+        if graph_steps > 0 and n >= graph_steps:
+            if self.steps_done == 0 and self.warm_first:
+                self.step(1)
+                n -= 1
+            if self.graph is None or self.graph_steps != graph_steps:
+                self.capture(graph_steps)
+            reps = n // graph_steps
+            self.replay(reps)
+            n -= reps * graph_steps
+        self.step(n)
+
+    # -- results --------------------------------------------------------------------
+    @property
+    def X(self) -> torch.Tensor:
+        return self.x[self.steps_done & 1]
+
+    @property
+    def u2_state(self) -> torch.Tensor:
+        return self.u2[self.steps_done & 1]
+
+    @property
+    def x2_state(self) -> torch.Tensor:
+        if self.alpha1:
+            return self.X
+        return self.x2[self.steps_done & 1]
+
+    def samples(self):
+        k = self.sched.n_samples_done(self.steps_done)
+        return self.sched.samples[:k] if k else self.sched.samples[:0] if self.sched.samples is not None else None
+
+    def blocks(self):
+        k = self.sched.n_blocks_done(self.steps_done)
+        if self.sched.blocks is None:
+            return None, None
+        return self.sched.blocks[:k], self.sched.blocks2[:k]

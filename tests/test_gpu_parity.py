@@ -1,0 +1,308 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the golden
+fixtures made by the reference itself.  Bit-exact where the kernel runs in EXACT mode or
+the op is integer / elementwise; the north-star tolerance (1e-5 relative, fp32, on the
+sample mean) for the fast TV kernels."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import psgla_oracle as orc
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+DEV = "cuda:0"
+
+# north-star tolerance on the sample mean (fp32): ||a - b|| / ||b|| <= 1e-5
+REL_TOL_MEAN = 1e-5
+
+
+def load(name):
+    return dict(np.load(os.path.join(G, name + ".npz"), allow_pickle=False))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from psgla_for_posterior_sampling_amd import _native as N
+    N.lib()
+    yield
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+# ------------------------------------------------------------------------------ noise
+def test_noise_tables_exhaustive():
+    """All 2^24 Box-Muller radii and all 2^24 angles: GPU == CPU checker, bit for bit."""
+    import ctypes
+    from psgla_for_posterior_sampling_amd import _native as N
+    n = 1 << 24
+    r = torch.empty(n, device=DEV)
+    c = torch.empty(n, device=DEV)
+    s = torch.empty(n, device=DEV)
+    N.check(N.lib().psgla_debug_bm_tables(r.data_ptr(), c.data_ptr(), s.data_ptr(), 0, n,
+                                          torch.cuda.current_stream().cuda_stream), "bm_tables")
+    torch.cuda.synchronize()
+    rr = orc.radius_table(0, n)
+    cc, ss = orc.angle_table(0, n)
+    np.testing.assert_array_equal(r.cpu().numpy(), rr)
+    np.testing.assert_array_equal(c.cpu().numpy(), cc)
+    np.testing.assert_array_equal(s.cpu().numpy(), ss)
+
+
+@pytest.mark.parametrize("shape,seed,chain0,step", [((1, 3, 24, 40), 0, 0, 0), ((3, 3, 17, 31), 5, 7, 123),
+                                                     ((2, 1, 5, 7), 2 ** 40 + 3, 0, 99999)])
+def test_normal_fill_matches_checker(shape, seed, chain0, step):
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    out = torch.empty(shape, device=DEV)
+    K.normal_fill(out, seed, chain0, step)
+    got = out.cpu()
+    for b in range(shape[0]):
+        ref = orc.normal((1,) + shape[1:], seed, chain0 + b, step)
+        assert torch.equal(got[b:b + 1], ref)
+
+
+# ------------------------------------------------------------------------------ TV prox
+def _tv_case(shape, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    y = torch.rand(shape, generator=g) + 0.05 * torch.randn(shape, generator=g)
+    return y
+
+
+@pytest.mark.parametrize("shape", [(1, 3, 24, 40), (2, 3, 70, 300), (1, 1, 5, 7), (1, 3, 33, 321)])
+@pytest.mark.parametrize("n_it", [10, 3])
+def test_tv_prox_exact_bitwise(shape, n_it):
+    from psgla_for_posterior_sampling_amd.denoisers import TVDenoiser
+    y = _tv_case(shape)
+    ths = torch.tensor(10 / 255.0, dtype=torch.float32)
+    ref = orc.TVDenoiser(n_it_max=n_it)
+    gpu = TVDenoiser(n_it_max=n_it, exact=True)
+    for call in range(3):   # first call restarts, later calls warm-start
+        yy = y + 0.01 * call
+        out_ref = ref.forward(yy, ths)
+        out = gpu.forward(yy.to(DEV), ths)
+        np.testing.assert_array_equal(out.cpu().numpy(), out_ref.numpy(), err_msg=f"call {call}")
+        np.testing.assert_array_equal(gpu.u2.cpu().numpy(), ref.u2.numpy())
+
+
+def test_tv_prox_early_stop_exact():
+    """tol large enough that deepinv's early stop fires: the finaliser must redo with k+1 its."""
+    from psgla_for_posterior_sampling_amd.denoisers import TVDenoiser
+    y = _tv_case((1, 3, 40, 52), seed=3)
+    ths = torch.tensor(10 / 255.0, dtype=torch.float32)
+    ref = orc.TVDenoiser(n_it_max=10, tol=3e-2)
+    gpu = TVDenoiser(n_it_max=10, tol=3e-2, exact=True)
+    out_ref = ref.forward(y, ths)
+    assert ref.last_n_it < 10, "test needs the early stop to fire"
+    out = gpu.forward(y.to(DEV), ths)
+    np.testing.assert_array_equal(out.cpu().numpy(), out_ref.numpy())
+
+
+@pytest.mark.parametrize("shape", [(1, 3, 24, 40), (2, 3, 130, 260)])
+def test_tv_prox_fast_tolerance(shape):
+    from psgla_for_posterior_sampling_amd.denoisers import TVDenoiser
+    y = _tv_case(shape, seed=1)
+    ths = torch.tensor(10 / 255.0, dtype=torch.float32)
+    ref = orc.TVDenoiser(n_it_max=10)
+    gpu = TVDenoiser(n_it_max=10, exact=False)
+    for call in range(3):
+        out_ref = ref.forward(y, ths)
+        out = gpu.forward(y.to(DEV), ths)
+        assert rel(out.cpu().numpy(), out_ref.numpy()) < 5e-6
+        assert np.abs(out.cpu().numpy() - out_ref.numpy()).max() < 1e-5
+
+
+# ------------------------------------------------------------------------------ fused PSGLA + TV
+def _run_fused_vs_fixture(exact):
+    from psgla_for_posterior_sampling_amd import restoration_algorithms as RA
+    from psgla_for_posterior_sampling_amd.denoisers import TVDenoiser
+    from psgla_for_posterior_sampling_amd.fidelity import InpaintingFidelity
+    fx = load("psgla_inpaint_tv")
+    seed, n, ni, nm, alpha, lam, s, delta, ntv = fx["meta"]
+    y = torch.from_numpy(fx["y"]).to(DEV)
+    mask = torch.from_numpy(fx["mask2d"]).to(DEV)
+    sigma2 = torch.tensor((1 / 255.0) ** 2, dtype=torch.float32)
+    dg = InpaintingFidelity(mask, y, sigma2)
+    tv = TVDenoiser(n_it_max=int(ntv), exact=exact)
+    out = RA.psgla(torch.from_numpy(fx["init"]).to(DEV), dg, tv, torch.tensor(alpha, dtype=torch.float32),
+                   torch.tensor(lam, dtype=torch.float32), sig_float=float(s), delta=float(delta),
+                   n_iter=int(n), n_inter=int(ni), n_inter_mmse=int(nm), seed=int(seed), graph_steps=20)
+    Xl, Ml, M2l = [np.stack([t.cpu().numpy() for t in lst]) for lst in out]
+    return fx, Xl, Ml, M2l, tv
+
+
+def test_fused_psgla_tv_exact_matches_reference_fixture():
+    fx, Xl, Ml, M2l, tv = _run_fused_vs_fixture(exact=True)
+    np.testing.assert_array_equal(Xl, fx["samples"])
+    np.testing.assert_array_equal(Ml, fx["blocks"])
+    np.testing.assert_array_equal(M2l, fx["blocks2"])
+    np.testing.assert_array_equal(tv.x2.cpu().numpy(), fx["tv_x2"])
+    np.testing.assert_array_equal(tv.u2.cpu().numpy(), fx["tv_u2"])
+
+
+def test_fused_psgla_tv_fast_within_tolerance():
+    fx, Xl, Ml, M2l, tv = _run_fused_vs_fixture(exact=False)
+    assert rel(Ml.mean(0), fx["blocks"].mean(0)) < REL_TOL_MEAN
+    assert rel(M2l.mean(0), fx["blocks2"].mean(0)) < REL_TOL_MEAN
+    assert Xl.shape == fx["samples"].shape
+
+
+def _fused_batch(B, chain0, exact, n_iter=40, H=48, W=64, alpha=1.0, y_shared=True):
+    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    g = torch.Generator().manual_seed(5)
+    x = torch.rand((1, 3, H, W), generator=g)
+    dg, y, init, mask2d = orc.inpainting_problem(x, seed_ip=1)
+    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
+    eng = FusedTvChains(init.expand(B, -1, -1, -1).contiguous().to(DEV), y.to(DEV),
+                        mask2d.to(torch.uint8).to(DEV), c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
+                        alpha=alpha, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10), seed=3,
+                        n_iter=n_iter, n_inter=5, n_inter_mmse=4, chain0=chain0, exact=exact)
+    return eng, (dg, y, init, mask2d, c1, c2)
+
+
+def test_fused_chains_independent_of_batching_and_graph():
+    """Chain k's trajectory depends only on (seed, global chain id): B=4 batch vs B=2 batch
+    with chain0=2, and eager vs hipGraph replay -- bit-identical (multi-GPU sharding property)."""
+    e4, _ = _fused_batch(4, 0, exact=False)
+    e4.run(40, graph_steps=0)
+    e2, _ = _fused_batch(2, 2, exact=False)
+    e2.run(40, graph_steps=10)
+    torch.cuda.synchronize()
+    assert torch.equal(e4.X[2:], e2.X)
+    b4, _ = e4.blocks()
+    b2, _ = e2.blocks()
+    assert torch.equal(b4[:, 2:], b2)
+    assert torch.equal(e4.samples()[:, 2:], e2.samples())
+
+
+def test_fused_multichain_exact_vs_oracle():
+    B = 3
+    eng, (dg, y, init, mask2d, c1, c2) = _fused_batch(B, 10, exact=True, n_iter=30)
+    eng.run(30, graph_steps=0)
+    torch.cuda.synchronize()
+    for b in range(B):
+        tv = orc.TVDenoiser(n_it_max=10)
+        Xl, Ml, M2l = orc.psgla(init, dg, tv, torch.tensor(1.0), torch.tensor(10.0), sig_float=10 / 255.0,
+                                delta=(10 / 255.0) ** 2, n_iter=30, n_inter=5, n_inter_mmse=4, seed=3,
+                                chain=10 + b)
+        np.testing.assert_array_equal(eng.samples()[:, b].cpu().numpy(), np.stack([t.numpy() for t in Xl]))
+        bm, bm2 = eng.blocks()
+        np.testing.assert_array_equal(bm[:, b].cpu().numpy(), np.stack([t.numpy() for t in Ml]))
+        np.testing.assert_array_equal(bm2[:, b].cpu().numpy(), np.stack([t.numpy() for t in M2l]))
+
+
+def test_fused_alpha_not_one_exact_vs_oracle():
+    eng, (dg, y, init, mask2d, c1, c2) = _fused_batch(1, 0, exact=True, n_iter=20, alpha=0.6)
+    eng.run(20)
+    torch.cuda.synchronize()
+    tv = orc.TVDenoiser(n_it_max=10)
+    Xl, Ml, M2l = orc.psgla(init, dg, tv, torch.tensor(0.6), torch.tensor(10.0), sig_float=10 / 255.0,
+                            delta=(10 / 255.0) ** 2, n_iter=20, n_inter=5, n_inter_mmse=4, seed=3, chain=0)
+    np.testing.assert_array_equal(eng.samples()[:, 0].cpu().numpy(), np.stack([t.numpy() for t in Xl]))
+    np.testing.assert_array_equal(eng.x2_state.cpu().numpy(), tv.x2.numpy())
+
+
+def test_fused_full_size_fast_vs_exact():
+    """BASELINE size (64 chains x 3x256x256), a few steps: fast vs exact kernels agree to fp32
+    rounding, no NaN, and the per-chain state stays bounded."""
+    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    g = torch.Generator(device=DEV).manual_seed(1234)
+    x = torch.rand((1, 3, 256, 256), generator=g, device=DEV)
+    from psgla_for_posterior_sampling_amd.fidelity import inpainting_problem
+    dg, y, init, mask2d, _ = inpainting_problem(x)
+    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
+    outs = []
+    for exact in (True, False):
+        eng = FusedTvChains(init.expand(64, -1, -1, -1).contiguous(), y, dg.mask_u8, c1=c1, c2=c2,
+                            sigma2=dg.sigma2, alpha=1.0, ths=float(np.float32(10 / 255.0)),
+                            tv=K.TvConstants(n_it_max=10), seed=0, n_iter=12, n_inter=10, n_inter_mmse=10,
+                            exact=exact)
+        eng.run(12, graph_steps=0)
+        torch.cuda.synchronize()
+        outs.append((eng.X.clone(), eng.blocks()[0].clone()))
+    (xe, be), (xf, bf) = outs
+    assert torch.isfinite(xf).all() and torch.isfinite(xe).all()
+    assert rel(bf.cpu().numpy(), be.cpu().numpy()) < REL_TOL_MEAN
+    assert rel(xf.cpu().numpy(), xe.cpu().numpy()) < 1e-4
+
+
+# ------------------------------------------------------------------------------ generic paths
+def test_generic_psgla_clamp_matches_reference_fixture():
+    from psgla_for_posterior_sampling_amd import restoration_algorithms as RA
+    fx = load("psgla_inpaint_clamp")
+    seed, n, ni, nm, alpha, lam, s, delta = fx["meta"]
+    y = torch.from_numpy(fx["y"]).to(DEV)
+    mask = torch.from_numpy(fx["mask2d"]).to(DEV)
+    from psgla_for_posterior_sampling_amd.fidelity import InpaintingFidelity
+    dg = InpaintingFidelity(mask, y, torch.tensor((1 / 255.0) ** 2, dtype=torch.float32))
+
+    class Clamp:
+        def forward(self, x, s):
+            return torch.clamp(x, 0.0, 1.0)
+    out = RA.psgla(torch.from_numpy(fx["init"]).to(DEV), dg, Clamp(), torch.tensor(alpha, dtype=torch.float32),
+                   torch.tensor(lam, dtype=torch.float32), sig_float=float(s), delta=float(delta),
+                   n_iter=int(n), n_inter=int(ni), n_inter_mmse=int(nm), seed=int(seed))
+    Xl, Ml, M2l = [np.stack([t.cpu().numpy() for t in lst]) for lst in out]
+    np.testing.assert_array_equal(Xl, fx["samples"])
+    np.testing.assert_array_equal(Ml, fx["blocks"])
+    np.testing.assert_array_equal(M2l, fx["blocks2"])
+
+
+def test_generic_psgla_alpha03_conv_matches_reference_fixture():
+    from psgla_for_posterior_sampling_amd import restoration_algorithms as RA
+    fx = load("psgla_inpaint_conv_alpha03")
+    seed, n, ni, nm, alpha, lam, s, delta = fx["meta"]
+    y = torch.from_numpy(fx["y"]).to(DEV)
+    mask = torch.from_numpy(fx["mask2d"]).to(DEV)
+    sigma2t = torch.tensor((1 / 255.0) ** 2, dtype=torch.float32, device=DEV)
+    mask4 = torch.ones(3, device=DEV)[None, :, None, None] * mask[None, None].long()
+    w = torch.from_numpy(fx["weight"]).to(DEV)
+    b = torch.from_numpy(fx["bias"]).to(DEV)
+
+    class Conv:
+        def forward(self, x, s):
+            return x - torch.nn.functional.conv2d(x, w, b, padding=1)
+    out = RA.psgla(torch.from_numpy(fx["init"]).to(DEV), lambda x: -mask4 * (x - y) / sigma2t, Conv(),
+                   torch.tensor(alpha, dtype=torch.float32), torch.tensor(lam, dtype=torch.float32),
+                   sig_float=float(s), delta=float(delta), n_iter=int(n), n_inter=int(ni),
+                   n_inter_mmse=int(nm), seed=int(seed))
+    Ml = np.stack([t.cpu().numpy() for t in out[1]])
+    # the conv runs in MIOpen on the GPU vs the CPU conv in the fixture: tolerance, not bits
+    assert rel(Ml.mean(0), fx["blocks"].mean(0)) < REL_TOL_MEAN
+
+
+def test_generic_pnpula_clamp_matches_reference_fixture():
+    from psgla_for_posterior_sampling_amd import restoration_algorithms as RA
+    from psgla_for_posterior_sampling_amd.fidelity import InpaintingFidelity
+    fx = load("pnpula_inpaint_clamp")
+    seed, n, ni, nm, alpha, lam, s1, delta = fx["meta"]
+    y = torch.from_numpy(fx["y"]).to(DEV)
+    mask = torch.from_numpy(fx["mask2d"]).to(DEV)
+    dg = InpaintingFidelity(mask, y, torch.tensor((1 / 255.0) ** 2, dtype=torch.float32))
+    s2t = torch.tensor(float(s1) ** 2, dtype=torch.float32, device=DEV)
+    alphat = torch.tensor(1.0, dtype=torch.float32, device=DEV)
+    out = RA.pnpula(torch.from_numpy(fx["init"]).to(DEV), dg, lambda x: alphat * (torch.clamp(x, 0, 1) - x) / s2t,
+                    torch.tensor(float(delta), dtype=torch.float32, device=DEV),
+                    torch.tensor(float(lam), dtype=torch.float32, device=DEV), n_iter=int(n), n_inter=int(ni),
+                    n_inter_mmse=int(nm), seed=int(seed))
+    Xl, Ml, M2l = [np.stack([t.cpu().numpy() for t in lst]) for lst in out]
+    np.testing.assert_array_equal(Xl, fx["samples"])
+    np.testing.assert_array_equal(Ml, fx["blocks"])
+    np.testing.assert_array_equal(M2l, fx["blocks2"])
+
+
+def test_inpaint_grad_bitwise():
+    from psgla_for_posterior_sampling_amd.fidelity import InpaintingFidelity
+    fx = load("psgla_inpaint_clamp")
+    dg_ref, y, init, mask2d = orc.inpainting_problem(torch.from_numpy(fx["x"]), seed_ip=0)
+    dg = InpaintingFidelity(mask2d.to(DEV), y.to(DEV), torch.tensor((1 / 255.0) ** 2, dtype=torch.float32))
+    x = torch.rand(init.shape)
+    np.testing.assert_array_equal(dg(x.to(DEV)).cpu().numpy(), dg_ref(x).numpy())

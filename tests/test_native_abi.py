@@ -1,0 +1,65 @@
+"""CPU-side checks of the C-ABI library: it loads without a GPU, exports every entry point
+declared in include/psgla_hip.h, and the ctypes descriptor layouts match the C structs."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "psgla_hip.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_the_entry_points():
+    fns = declared_functions()
+    for f in ("psgla_tv_step", "psgla_tv_prox", "psgla_langevin_update", "psgla_relax_accumulate",
+              "pnpula_update", "psgla_normal_fill", "psgla_inpaint_grad", "psgla_abi_version"):
+        assert f in fns
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    from psgla_for_posterior_sampling_amd import _native as N
+    lib = N.lib()
+    for f in declared_functions():
+        assert hasattr(lib, f), f
+        assert f in N.EXPORTED_SYMBOLS, f"{f} not bound in _native"
+    assert lib.psgla_abi_version() == N.ABI_VERSION
+
+
+def test_struct_layouts_match_c(tmp_path):
+    from psgla_for_posterior_sampling_amd import _native as N
+    prog = tmp_path / "sz.c"
+    fields = {"PsglaTvStep": [f[0] for f in N.PsglaTvStep._fields_],
+              "PsglaSchedule": [f[0] for f in N.PsglaSchedule._fields_],
+              "PsglaTvProx": [f[0] for f in N.PsglaTvProx._fields_]}
+    lines = ['#include "psgla_hip.h"', "#include <stdio.h>", "#include <stddef.h>", "int main(void){"]
+    for s, fs in fields.items():
+        lines.append(f'printf("{s} %zu\\n", sizeof({s}));')
+        for f in fs:
+            lines.append(f'printf("{s}.{f} %zu\\n", offsetof({s}, {f}));')
+    lines.append("return 0;}")
+    prog.write_text("\n".join(lines))
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(prog), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = dict(l.rsplit(" ", 1) for l in out if l)
+    for s in fields:
+        cls = getattr(N, s)
+        assert int(got[s]) == ctypes.sizeof(cls), s
+        for f in fields[s]:
+            assert int(got[f"{s}.{f}"]) == getattr(cls, f).offset, f"{s}.{f}"
+
+
+def test_no_cpu_fallback_without_library(monkeypatch):
+    from psgla_for_posterior_sampling_amd import _native as N
+    monkeypatch.setattr(N, "_lib", None)
+    monkeypatch.setattr(N, "LIB_PATH", "/nonexistent/libpsgla_hip.so")
+    with pytest.raises(N.NativeLibraryError):
+        N.lib()
