@@ -99,6 +99,8 @@ typedef struct PsglaTvStep {
     int32_t* arrive;          /* device int, zero-initialised (finaliser arrival counter)   */
     int32_t launch_mask;      /* 0 or 3: both kernels; 1: tile kernel only (re-runs the same step:
                                  idempotent, for kernel timing); 2: finaliser only            */
+    int32_t kernel_variant;   /* 0: auto (row-streaming pipeline when W % 4 == 0 and n_tv <= 10,
+                                 else temporally blocked bands); 1: force bands; 2: force stream */
 } PsglaTvStep;
 
 int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream);

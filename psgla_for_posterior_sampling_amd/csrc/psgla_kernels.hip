@@ -84,6 +84,7 @@ struct TvArgs {
     long long blocks_cap;
     // tiling
     int nbands, band_h, nsegs, seg_w, tiles, halo;
+    int stream;                     // 1: main pass = row-streaming pipeline kernel
 };
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -506,6 +507,347 @@ __global__ void __launch_bounds__(TV_THREADS) tv_finalise_kernel(const TvArgs a)
 }
 
 // ---------------------------------------------------------------------------------------
+// Row-streaming pipeline: the production PSGLA+TV step for W % 4 == 0 and n_tv <= 10.
+//
+// One workgroup streams one (chain, channel) plane -- or a <=256-column segment of it, with
+// a horizontal halo of n_tv columns -- from top to bottom, one row per pipeline step:
+//   waves 0-3   FRONT: row r is owned by wave r % 4 and processed over 4 steps (software
+//               pipelined): Philox, Box-Muller pair 1, pair 2, then the data term
+//               Y = (X + c1 g) + c2 Z and the TV state (x2, u2) are written to LDS ring 0;
+//               the global loads of the wave's next row are issued 4 steps ahead.
+//   waves 4..   STAGE k = 1..n_tv (one wave per inner TV iteration): at step t it computes
+//               the primal update of row j = t-2-2k and the dual update of row i = j-1 from
+//               ring k-1 (written one step earlier) and writes (x2, u2) of row i to ring k.
+//               Row i's dual update needs z of rows i and i+1, hence the lag of 2 per stage.
+//   last 2      BACK: X = x2 (or the alpha relaxation), block accumulators, sample / block
+//               slots, chain state out; mean/sq loads prefetched 2 rows ahead.
+// All waves meet at one barrier per step.  Compared with the band kernel there is no
+// vertical halo recompute, and the HBM loads / stores of every row overlap the TV
+// iterations of the rows in flight (the band kernel runs load -> compute -> store in
+// lockstep on every CU).
+// ---------------------------------------------------------------------------------------
+constexpr int SP_FRONT = 4;
+constexpr int SP_BACK = 2;
+constexpr int SP_MAXST = 10;
+constexpr int SP_YRING = 32;
+
+struct StreamShared {
+    float4 x2[SP_MAXST + 1][2][WAVE];     // ring k = output of stage k (k = 0: front), 2 row slots
+    float4 u0[SP_MAXST + 1][2][WAVE];
+    float4 u1[SP_MAXST + 1][2][WAVE];
+    float4 y[SP_YRING][WAVE];             // Y rows (prox anchor), alive from the front to the back
+    float red[SP_MAXST][2];
+};
+
+struct StepInfo {
+    bool acc, first, blockend, liveout, sample;
+    long long blk, sidx;
+    float ca, cb;
+};
+
+__device__ __forceinline__ StepInfo step_info(const TvArgs& a, long long step, const float* mean_out) {
+    StepInfo si;
+    si.acc = a.nm >= 0 && mean_out != nullptr;
+    const int per = a.nm + 1;
+    const int im = si.acc ? (int)(step % per) : 0;
+    si.first = im == 0;
+    si.blk = si.acc ? step / per : 0;
+    si.liveout = si.acc && im != a.nm;
+    si.blockend = si.acc && im == a.nm && si.blk < a.blocks_cap;
+    si.ca = si.acc ? a.coef[2 * im] : 0.f;
+    si.cb = si.acc ? a.coef[2 * im + 1] : 0.f;
+    si.sample = a.n_inter > 0 && a.samples != nullptr && (step % a.n_inter) == 0;
+    si.sidx = si.sample ? step / a.n_inter : 0;
+    si.sample = si.sample && si.sidx < a.samples_cap;
+    return si;
+}
+
+template <bool EXACT, bool ALPHA1>
+__global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
+    __shared__ StreamShared sh;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int w = threadIdx.x >> 6;
+    const int n = a.n_tv;
+    const int H = a.H, W = a.W, C = a.C;
+    const long long step = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
+    const bool fresh = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
+    const int plane = blockIdx.x / a.nsegs;
+    const int seg = blockIdx.x - plane * a.nsegs;
+    const int b = plane / C, c = plane - b * C;
+    const int cc0 = seg * a.seg_w, cc1 = min(W, cc0 + a.seg_w);
+    const int f0 = max(0, cc0 - a.halo) & ~3;
+    const int gj0 = f0 + CPL * lane;
+    const bool lane_ok = gj0 < W;
+    const bool core = lane_ok && gj0 >= cc0 && gj0 < cc1;   // W % 4 == 0: a lane's 4 columns are all core or none
+    const size_t HW = (size_t)H * W;
+    const size_t E = (size_t)C * HW;
+    const size_t BE = (size_t)a.B * E;
+    const size_t plane_off = (size_t)b * E + (size_t)c * HW;
+    const int par_in = (int)(step & 1), par_out = (int)((step + 1) & 1);
+    bool hasLeft[CPL], hasRight[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        hasLeft[k] = gj0 + k > 0;
+        hasRight[k] = gj0 + k < W - 1;
+    }
+    const int nsteps = H + 4 + 2 * n;
+    const int role = (w < SP_FRONT) ? 0 : (w < SP_FRONT + n ? 1 : 2);
+    const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+
+    float sd = 0.f, sn = 0.f;
+    const int k_st = w - SP_FRONT + 1;                 // inner TV iteration (1-based)
+    const bool trk = role == 1 && (k_st - 1) >= 2 && (k_st - 1) <= n - 2;
+    // Each role runs its own loop (its state is live only there); every wave executes
+    // exactly nsteps barriers, so the s_barrier instances pair up across roles.
+    if (role == 0) {
+        // ---------------- FRONT state ----------------
+        const int fw = w;                                  // front wave id (rows r % 4 == fw)
+        float4 fX = zero4, fU0 = zero4, fU1 = zero4, fXS = zero4, fYo = zero4;
+        uchar4 fM = make_uchar4(0, 0, 0, 0);
+        uint32_t ph0 = 0, ph1 = 0, ph2 = 0, ph3 = 0;
+        float zn0 = 0.f, zn1 = 0.f, zn2 = 0.f, zn3 = 0.f;
+        const float* xin = a.x[par_in];
+        const float* u2in = a.u2[par_in];
+        const float* x2in = ALPHA1 ? nullptr : a.x2[par_in];
+        auto front_issue = [&](int r) {
+            if (r < H && lane_ok) {
+                const size_t base = plane_off + (size_t)r * W + gj0;
+                fX = ld4(xin + base);
+                fYo = ld4(a.yobs + (size_t)b * a.y_cs + (size_t)c * HW + (size_t)r * W + gj0);
+                fM = *reinterpret_cast<const uchar4*>(a.mask + (size_t)b * a.m_cs + (size_t)r * W + gj0);
+                if (!fresh) {
+                    fU0 = ld4(u2in + 2 * base);
+                    fU1 = ld4(u2in + 2 * base + 4);
+                    if (!ALPHA1) fXS = ld4(x2in + base);
+                }
+            }
+        };
+
+        front_issue(fw);
+        for (int t = 0; t < nsteps; ++t) {
+                // ======================= FRONT =======================
+                const int p = (t + 4 - fw) & 3;
+                const int r = t - p;
+                if (r >= 0 && r < H) {
+                    if (p == 0) {
+                        const size_t e = ((size_t)c * H + r) * W + gj0;
+                        uint32_t c0 = (uint32_t)(e >> 2), c1 = (uint32_t)step, c2 = TAG_LANGEVIN,
+                                 c3 = (uint32_t)(a.seed >> 32);
+                        philox4x32_10(c0, c1, c2, c3, (uint32_t)a.seed, (uint32_t)(a.chain0 + b));
+                        ph0 = c0; ph1 = c1; ph2 = c2; ph3 = c3;
+                    } else if (p == 1) {
+                        box_muller(ph0, ph1, zn0, zn1);
+                    } else if (p == 2) {
+                        box_muller(ph2, ph3, zn2, zn3);
+                    } else {
+                        const float X[CPL] = {fX.x, fX.y, fX.z, fX.w};
+                        const float yo[CPL] = {fYo.x, fYo.y, fYo.z, fYo.w};
+                        const float mk[CPL] = {(float)fM.x, (float)fM.y, (float)fM.z, (float)fM.w};
+                        const float Z[CPL] = {zn0, zn1, zn2, zn3};
+                        float Yv[CPL];
+#pragma unroll
+                        for (int k = 0; k < CPL; ++k) {
+                            const float g = (-mk[k] * (X[k] - yo[k])) / a.sigma2;
+                            Yv[k] = lane_ok ? (X[k] + a.c1 * g) + a.c2 * Z[k] : 0.f;
+                        }
+                        const float4 Y4 = make_float4(Yv[0], Yv[1], Yv[2], Yv[3]);
+                        float4 x2s;
+                        if (fresh) x2s = Y4;
+                        else x2s = ALPHA1 ? fX : fXS;
+                        if (!lane_ok) x2s = zero4;
+                        const int s0 = r & 1;
+                        sh.x2[0][s0][lane] = x2s;
+                        sh.u0[0][s0][lane] = fresh ? zero4 : make_float4(fU0.x, fU0.z, fU1.x, fU1.z);
+                        sh.u1[0][s0][lane] = fresh ? zero4 : make_float4(fU0.y, fU0.w, fU1.y, fU1.w);
+                        sh.y[r & (SP_YRING - 1)][lane] = Y4;
+                        front_issue(r + 4);
+                    }
+                }
+            __syncthreads();
+        }
+    } else if (role == 1) {
+        // ---------------- STAGE state ----------------
+        float pu0[CPL], pu1[CPL], zi[CPL], x2i[CPL];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) { pu0[k] = 0.f; pu1[k] = 0.f; zi[k] = 0.f; x2i[k] = 0.f; }
+
+        for (int t = 0; t < nsteps; ++t) {
+                // ======================= STAGE k =======================
+                const int k = k_st;
+                const int j = t - 2 - 2 * k;
+                const int i = j - 1;
+                const bool jv = j >= 0 && j < H;
+                const bool iv = i >= 0 && i < H;
+                float zj[CPL], x2nj[CPL], u0o[CPL], u1o[CPL];
+                if (jv) {
+                    const int sl = j & 1;
+                    const float4 X2 = sh.x2[k - 1][sl][lane];
+                    const float4 U0 = sh.u0[k - 1][sl][lane];
+                    const float4 U1 = sh.u1[k - 1][sl][lane];
+                    const float4 YY = sh.y[j & (SP_YRING - 1)][lane];
+                    const float x2o[CPL] = {X2.x, X2.y, X2.z, X2.w};
+                    u0o[0] = U0.x; u0o[1] = U0.y; u0o[2] = U0.z; u0o[3] = U0.w;
+                    u1o[0] = U1.x; u1o[1] = U1.y; u1o[2] = U1.z; u1o[3] = U1.w;
+                    const float yy[CPL] = {YY.x, YY.y, YY.z, YY.w};
+                    const float u1l = __shfl_up(u1o[CPL - 1], 1);
+                    const bool dn = j < H - 1, upv = j > 0;
+#pragma unroll
+                    for (int kk = 0; kk < CPL; ++kk) {
+                        const float u1left = kk > 0 ? u1o[kk - 1] : u1l;
+                        float tt = dn ? (0.0f - u0o[kk]) : 0.0f;
+                        tt = upv ? tt + pu0[kk] : tt;
+                        tt = hasRight[kk] ? tt - u1o[kk] : tt;
+                        tt = hasLeft[kk] ? tt + u1left : tt;
+                        const float xo = x2o[kk];
+                        float xv, zv, xn;
+                        if (EXACT) {
+                            xv = ((xo - a.tau * tt) + a.tau * yy[kk]) / a.opt;
+                            zv = 2.0f * xv - xo;
+                            xn = xo + a.rho * (xv - xo);
+                        } else {
+                            xv = __builtin_fmaf(a.tau, yy[kk] - tt, xo) * a.inv_opt;
+                            zv = __builtin_fmaf(2.0f, xv, -xo);
+                            xn = __builtin_fmaf(a.rho, xv - xo, xo);
+                        }
+                        if (trk && core) {
+                            const float d = xo - xn;
+                            const float q = xn + 1e-12f;
+                            sd += d * d;
+                            sn += q * q;
+                        }
+                        zj[kk] = zv;
+                        x2nj[kk] = xn;
+                    }
+                }
+                if (iv) {
+                    const float zr3 = __shfl_down(zi[0], 1);
+                    const bool dn = i < H - 1;
+                    float un0[CPL], un1[CPL];
+#pragma unroll
+                    for (int kk = 0; kk < CPL; ++kk) {
+                        const float zc = zi[kk];
+                        const float zd = jv ? zj[kk] : 0.f;
+                        const float zr = kk < CPL - 1 ? zi[kk + 1] : zr3;
+                        const float g0 = dn ? ((0.0f - zc) + zd) : 0.0f;
+                        const float g1 = hasRight[kk] ? ((0.0f - zc) + zr) : 0.0f;
+                        const float uo0 = pu0[kk], uo1 = pu1[kk];
+                        if (EXACT) {
+                            const float v0 = uo0 + a.sig_tv * g0;
+                            const float v1 = uo1 + a.sig_tv * g1;
+                            const float nrm = sqrtf(v0 * v0 + v1 * v1) / a.ths;
+                            const float dd = fmaxf(nrm, 1.0f);
+                            un0[kk] = uo0 + a.rho * (v0 / dd - uo0);
+                            un1[kk] = uo1 + a.rho * (v1 / dd - uo1);
+                        } else {
+                            const float v0 = __builtin_fmaf(a.sig_tv, g0, uo0);
+                            const float v1 = __builtin_fmaf(a.sig_tv, g1, uo1);
+                            const float s2 = __builtin_fmaf(v0, v0, v1 * v1);
+                            const float f = fminf(1.0f, a.ths * __builtin_amdgcn_rsqf(s2));
+                            un0[kk] = __builtin_fmaf(a.rho, __builtin_fmaf(v0, f, -uo0), uo0);
+                            un1[kk] = __builtin_fmaf(a.rho, __builtin_fmaf(v1, f, -uo1), uo1);
+                        }
+                    }
+                    const int so = i & 1;
+                    sh.x2[k][so][lane] = make_float4(x2i[0], x2i[1], x2i[2], x2i[3]);
+                    sh.u0[k][so][lane] = make_float4(un0[0], un0[1], un0[2], un0[3]);
+                    sh.u1[k][so][lane] = make_float4(un1[0], un1[1], un1[2], un1[3]);
+                }
+                if (jv) {
+#pragma unroll
+                    for (int kk = 0; kk < CPL; ++kk) {
+                        pu0[kk] = u0o[kk]; pu1[kk] = u1o[kk]; zi[kk] = zj[kk]; x2i[kk] = x2nj[kk];
+                    }
+                }
+            __syncthreads();
+        }
+    } else {
+        // ---------------- BACK state ----------------
+        const int bw = w - SP_FRONT - n;                   // back wave id (rows r % 2 == bw)
+        const StepInfo si = step_info(a, step, a.mean[par_out]);
+        float4 bm = zero4, bq = zero4;
+        const float* mean_in = a.mean[par_in];
+        const float* sq_in = a.sq[par_in];
+        auto back_issue = [&](int r) {
+            if (r < H && core && si.acc && !si.first) {
+                const size_t base = plane_off + (size_t)r * W + gj0;
+                bm = ld4(mean_in + base);
+                bq = ld4(sq_in + base);
+            }
+        };
+
+        back_issue(bw);
+        for (int t = 0; t < nsteps; ++t) {
+                // ======================= BACK =======================
+                const int r = t - 4 - 2 * n;
+                if (r >= 0 && r < H && (r & 1) == bw) {
+                    const int sl = r & 1;
+                    const float4 X2 = sh.x2[n][sl][lane];
+                    const float4 U0 = sh.u0[n][sl][lane];
+                    const float4 U1 = sh.u1[n][sl][lane];
+                    float4 Xo = X2;
+                    if (!ALPHA1) {
+                        const float4 YY = sh.y[r & (SP_YRING - 1)][lane];
+                        Xo.x = (1.0f - a.alpha) * YY.x + a.alpha * X2.x;
+                        Xo.y = (1.0f - a.alpha) * YY.y + a.alpha * X2.y;
+                        Xo.z = (1.0f - a.alpha) * YY.z + a.alpha * X2.z;
+                        Xo.w = (1.0f - a.alpha) * YY.w + a.alpha * X2.w;
+                    }
+                    if (core) {
+                        const size_t base = plane_off + (size_t)r * W + gj0;
+                        *reinterpret_cast<float4*>(a.x[par_out] + base) = Xo;
+                        float* u2o = a.u2[par_out] + 2 * base;
+                        *reinterpret_cast<float4*>(u2o) = make_float4(U0.x, U1.x, U0.y, U1.y);
+                        *reinterpret_cast<float4*>(u2o + 4) = make_float4(U0.z, U1.z, U0.w, U1.w);
+                        if (!ALPHA1) *reinterpret_cast<float4*>(a.x2[par_out] + base) = X2;
+                        if (si.acc) {
+                            const float xs[CPL] = {Xo.x, Xo.y, Xo.z, Xo.w};
+                            const float ms[CPL] = {bm.x, bm.y, bm.z, bm.w};
+                            const float qs[CPL] = {bq.x, bq.y, bq.z, bq.w};
+                            float m[CPL], q[CPL];
+#pragma unroll
+                            for (int kk = 0; kk < CPL; ++kk) {
+                                if (si.first) {
+                                    m[kk] = si.cb * xs[kk];
+                                    q[kk] = si.cb * (xs[kk] * xs[kk]);
+                                } else {
+                                    m[kk] = si.ca * ms[kk] + si.cb * xs[kk];
+                                    q[kk] = si.ca * qs[kk] + si.cb * (xs[kk] * xs[kk]);
+                                }
+                            }
+                            const float4 M4 = make_float4(m[0], m[1], m[2], m[3]);
+                            const float4 Q4 = make_float4(q[0], q[1], q[2], q[3]);
+                            if (si.blockend) {
+                                *reinterpret_cast<float4*>(a.blocks + (size_t)si.blk * BE + base) = M4;
+                                *reinterpret_cast<float4*>(a.blocks2 + (size_t)si.blk * BE + base) = Q4;
+                            } else if (si.liveout) {
+                                *reinterpret_cast<float4*>(a.mean[par_out] + base) = M4;
+                                *reinterpret_cast<float4*>(a.sq[par_out] + base) = Q4;
+                            }
+                        }
+                        if (si.sample) *reinterpret_cast<float4*>(a.samples + (size_t)si.sidx * BE + base) = Xo;
+                    }
+                    back_issue(r + 2);
+                }
+            __syncthreads();
+        }
+    }
+
+    // rel_err partial sums of this plane -> global (deepinv's early-stop test, per chain)
+    if (role == 1 && trk) {
+        sd = wave_sum(sd);
+        sn = wave_sum(sn);
+        if (lane == 0) { sh.red[k_st - 1][0] = sd; sh.red[k_st - 1][1] = sn; }
+    }
+    __syncthreads();
+    if (threadIdx.x >= 2 && (int)threadIdx.x <= n - 2) {
+        const int tt = threadIdx.x;
+        const int g = a.per_chain_norm ? b : 0;
+        atomicAdd(&a.norms[((size_t)g * a.n_tv + tt) * 2], (double)sh.red[tt][0]);
+        atomicAdd(&a.norms[((size_t)g * a.n_tv + tt) * 2 + 1], (double)sh.red[tt][1]);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // Generic elementwise kernels (opaque closures; also the first / last steps of fused paths)
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ long long read_step(const long long* d, long long off) {
@@ -721,8 +1063,23 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
     const int P = a.B * a.C;
     if (mask == 0) mask = 3;
     if (mask & 1) {
-        const int grid_main = ((P + 7) / 8) * 8 * a.tiles;
-        hipLaunchKernelGGL((tv_main_kernel<EXACT, FRONT, ALPHA1>), dim3(grid_main), dim3(TV_THREADS), 0, st, a);
+        if (FRONT == FRONT_INPAINT && a.stream) {
+            TvArgs s = a;
+            s.halo = a.n_tv;
+            s.nbands = 1;
+            s.band_h = a.H;
+            if (a.W <= TV_COLS) { s.seg_w = a.W; s.nsegs = 1; }
+            else {
+                const int sw = (TV_COLS - 2 * s.halo - 3) & ~3;
+                s.nsegs = (a.W + sw - 1) / sw;
+                s.seg_w = (((a.W + s.nsegs - 1) / s.nsegs) + 3) & ~3;
+            }
+            const int threads = WAVE * (SP_FRONT + a.n_tv + SP_BACK);
+            hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1>), dim3(P * s.nsegs), dim3(threads), 0, st, s);
+        } else {
+            const int grid_main = ((P + 7) / 8) * 8 * a.tiles;
+            hipLaunchKernelGGL((tv_main_kernel<EXACT, FRONT, ALPHA1>), dim3(grid_main), dim3(TV_THREADS), 0, st, a);
+        }
         int rc = launch_check("tv_kernel(main)");
         if (rc) return rc;
     }
@@ -776,6 +1133,9 @@ int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream) {
     a.blocks = s->blocks; a.blocks2 = s->blocks2; a.blocks_cap = s->blocks_cap;
     a.halo = d->n_tv;
     tv_tiling(a);
+    const bool streamable = (d->W % 4 == 0) && d->n_tv >= 1 && d->n_tv <= SP_MAXST && d->H >= 2;
+    a.stream = streamable && d->kernel_variant != 1;
+    if (d->kernel_variant == 2 && !streamable) return fail(0, "psgla_tv_step: shape not supported by the streaming kernel");
     hipStream_t st = (hipStream_t)stream;
     const int m = d->launch_mask;
     if (d->exact)

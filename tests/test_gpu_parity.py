@@ -153,7 +153,7 @@ def test_fused_psgla_tv_fast_within_tolerance():
     assert Xl.shape == fx["samples"].shape
 
 
-def _fused_batch(B, chain0, exact, n_iter=40, H=48, W=64, alpha=1.0, y_shared=True):
+def _fused_batch(B, chain0, exact, n_iter=40, H=48, W=64, alpha=1.0, variant="auto"):
     from psgla_for_posterior_sampling_amd.engine import FusedTvChains
     from psgla_for_posterior_sampling_amd import hip_ops as K
     g = torch.Generator().manual_seed(5)
@@ -163,16 +163,18 @@ def _fused_batch(B, chain0, exact, n_iter=40, H=48, W=64, alpha=1.0, y_shared=Tr
     eng = FusedTvChains(init.expand(B, -1, -1, -1).contiguous().to(DEV), y.to(DEV),
                         mask2d.to(torch.uint8).to(DEV), c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
                         alpha=alpha, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10), seed=3,
-                        n_iter=n_iter, n_inter=5, n_inter_mmse=4, chain0=chain0, exact=exact)
+                        n_iter=n_iter, n_inter=5, n_inter_mmse=4, chain0=chain0, exact=exact,
+                        kernel_variant=variant)
     return eng, (dg, y, init, mask2d, c1, c2)
 
 
-def test_fused_chains_independent_of_batching_and_graph():
+@pytest.mark.parametrize("variant", ["stream", "band"])
+def test_fused_chains_independent_of_batching_and_graph(variant):
     """Chain k's trajectory depends only on (seed, global chain id): B=4 batch vs B=2 batch
     with chain0=2, and eager vs hipGraph replay -- bit-identical (multi-GPU sharding property)."""
-    e4, _ = _fused_batch(4, 0, exact=False)
+    e4, _ = _fused_batch(4, 0, exact=False, variant=variant)
     e4.run(40, graph_steps=0)
-    e2, _ = _fused_batch(2, 2, exact=False)
+    e2, _ = _fused_batch(2, 2, exact=False, variant=variant)
     e2.run(40, graph_steps=10)
     torch.cuda.synchronize()
     assert torch.equal(e4.X[2:], e2.X)
@@ -182,9 +184,11 @@ def test_fused_chains_independent_of_batching_and_graph():
     assert torch.equal(e4.samples()[:, 2:], e2.samples())
 
 
-def test_fused_multichain_exact_vs_oracle():
+@pytest.mark.parametrize("variant,H,W", [("stream", 48, 64), ("band", 48, 64), ("stream", 70, 300),
+                                          ("band", 70, 300), ("auto", 37, 29)])
+def test_fused_multichain_exact_vs_oracle(variant, H, W):
     B = 3
-    eng, (dg, y, init, mask2d, c1, c2) = _fused_batch(B, 10, exact=True, n_iter=30)
+    eng, (dg, y, init, mask2d, c1, c2) = _fused_batch(B, 10, exact=True, n_iter=30, H=H, W=W, variant=variant)
     eng.run(30, graph_steps=0)
     torch.cuda.synchronize()
     for b in range(B):
@@ -198,8 +202,9 @@ def test_fused_multichain_exact_vs_oracle():
         np.testing.assert_array_equal(bm2[:, b].cpu().numpy(), np.stack([t.numpy() for t in M2l]))
 
 
-def test_fused_alpha_not_one_exact_vs_oracle():
-    eng, (dg, y, init, mask2d, c1, c2) = _fused_batch(1, 0, exact=True, n_iter=20, alpha=0.6)
+@pytest.mark.parametrize("variant", ["stream", "band"])
+def test_fused_alpha_not_one_exact_vs_oracle(variant):
+    eng, (dg, y, init, mask2d, c1, c2) = _fused_batch(1, 0, exact=True, n_iter=20, alpha=0.6, variant=variant)
     eng.run(20)
     torch.cuda.synchronize()
     tv = orc.TVDenoiser(n_it_max=10)
@@ -220,15 +225,16 @@ def test_fused_full_size_fast_vs_exact():
     dg, y, init, mask2d, _ = inpainting_problem(x)
     c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
     outs = []
-    for exact in (True, False):
+    for exact, variant in ((True, "stream"), (False, "stream"), (True, "band")):
         eng = FusedTvChains(init.expand(64, -1, -1, -1).contiguous(), y, dg.mask_u8, c1=c1, c2=c2,
                             sigma2=dg.sigma2, alpha=1.0, ths=float(np.float32(10 / 255.0)),
                             tv=K.TvConstants(n_it_max=10), seed=0, n_iter=12, n_inter=10, n_inter_mmse=10,
-                            exact=exact)
+                            exact=exact, kernel_variant=variant)
         eng.run(12, graph_steps=0)
         torch.cuda.synchronize()
         outs.append((eng.X.clone(), eng.blocks()[0].clone()))
-    (xe, be), (xf, bf) = outs
+    (xe, be), (xf, bf), (xb, bb) = outs
+    assert torch.equal(xe, xb) and torch.equal(be, bb)      # both exact kernels agree bit for bit
     assert torch.isfinite(xf).all() and torch.isfinite(xe).all()
     assert rel(bf.cpu().numpy(), be.cpu().numpy()) < REL_TOL_MEAN
     assert rel(xf.cpu().numpy(), xe.cpu().numpy()) < 1e-4
