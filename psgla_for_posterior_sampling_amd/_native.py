@@ -10,7 +10,7 @@ import ctypes
 import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "libpsgla_hip.so")
+LIB_PATH = os.environ.get("PSGLA_LIB", os.path.join(_PKG, "libpsgla_hip.so"))
 ABI_VERSION = 1
 TV_MAX_FUSED_IT = 24
 

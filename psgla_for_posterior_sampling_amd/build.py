@@ -3,6 +3,7 @@
     hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared -I include \
           -o psgla_for_posterior_sampling_amd/libpsgla_hip.so csrc/psgla_kernels.hip
 
+-fno-slp-vectorize: packed fp32 (v_pk_*) needs operand shuffles and measured slower on gfx950.
 -ffp-contract=off keeps the reference's separate multiply/add roundings (the EXACT
 kernels are bit-identical to the torch CPU checker); fmas are written explicitly
 where the fast kernels want them.
@@ -35,16 +36,17 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(s) <= t for s in SOURCES + HEADERS)
 
 
-def build_native(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
+def build_native(force: bool = False, verbose: bool = False, out: str = OUT) -> str:
+    if not force and out == OUT and up_to_date():
         return OUT
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
-           "-shared", "-I", os.path.join(REPO, "include"), "-o", OUT + ".tmp"] + SOURCES
+    extra = os.environ.get("PSGLA_HIPCC_EXTRA", "").split()
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-fPIC",
+           "-shared", "-I", os.path.join(REPO, "include"), "-o", out + ".tmp"] + extra + SOURCES
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

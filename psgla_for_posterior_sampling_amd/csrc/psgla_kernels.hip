@@ -536,8 +536,30 @@ struct StreamShared {
     float4 u0[SP_MAXST + 1][2][WAVE];
     float4 u1[SP_MAXST + 1][2][WAVE];
     float4 y[SP_YRING][WAVE];             // Y rows (prox anchor), alive from the front to the back
+    // LDS-DMA staging (global_load_lds_dwordx4): a front wave's next row (X, y, u2 lo/hi, x2)
+    // and a back wave's next mean/sq rows land here without occupying VGPRs.
+    float4 fst[SP_FRONT][2][5][WAVE];
+    uint32_t fmk[SP_FRONT][2][WAVE];
+    float4 bst[SP_BACK][2][2][WAVE];
     float red[SP_MAXST][2];
 };
+
+typedef __attribute__((address_space(1))) const void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+// 16 B (4 B) per lane from global memory straight into LDS; lane i lands at dst + 16 i (4 i).
+__device__ __forceinline__ void glds16(const void* src, void* dst) {
+    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void* src, void* dst) {
+    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 4, 0, 0);
+}
+// Workgroup barrier that only drains LDS (lgkmcnt): LDS-DMA loads stay in flight across it
+// (a __syncthreads() fence would wait vmcnt(0) while a global_load_lds is pending).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 struct StepInfo {
     bool acc, first, blockend, liveout, sample;
@@ -562,11 +584,151 @@ __device__ __forceinline__ StepInfo step_info(const TvArgs& a, long long step, c
     return si;
 }
 
+// One pipeline stage = one inner TV iteration on one row pair.  Phase A (primal) on the
+// lookahead row j from ring k-1; phase B (dual) on the output row i = j-1, which needs z of
+// rows i (held from the previous step) and j.
+struct StageRow {
+    float u0[CPL], u1[CPL];   // u2^{k-1} of the row
+    float z[CPL];             // z^k of the row
+    float x2n[CPL];           // x2^k of the row
+};
+
+template <bool EXACT, bool TRK>
+__device__ __forceinline__ void stage_phase_a(const TvArgs& a, const float4& X2, const float4& U0,
+                                              const float4& U1, const float4& YY, const float (&pu0)[CPL],
+                                              StageRow& o, float& sd, float& sn) {
+    const float x2o[CPL] = {X2.x, X2.y, X2.z, X2.w};
+    const float yy[CPL] = {YY.x, YY.y, YY.z, YY.w};
+    o.u0[0] = U0.x; o.u0[1] = U0.y; o.u0[2] = U0.z; o.u0[3] = U0.w;
+    o.u1[0] = U1.x; o.u1[1] = U1.y; o.u1[2] = U1.z; o.u1[3] = U1.w;
+    // u1 of the column left of this lane's first column (lane-1's last); 0 at lane 0
+    const float u1l = __int_as_float(
+        __builtin_amdgcn_update_dpp(0, __float_as_int(o.u1[CPL - 1]), 0x138 /* wave_shr:1 */, 0xF, 0xF, true));
+#pragma unroll
+    for (int kk = 0; kk < CPL; ++kk) {
+        const float u1left = kk > 0 ? o.u1[kk - 1] : u1l;
+        // nabla^T u2 in deepinv's order: (((0 - u0) + u0[i-1]) - u1) + u1[j-1]
+        const float tt = (((0.0f - o.u0[kk]) + pu0[kk]) - o.u1[kk]) + u1left;
+        const float xo = x2o[kk];
+        float xv, zv, xn;
+        if (EXACT) {
+            xv = ((xo - a.tau * tt) + a.tau * yy[kk]) / a.opt;
+            zv = 2.0f * xv - xo;
+            xn = xo + a.rho * (xv - xo);
+        } else {
+            xv = __builtin_fmaf(a.tau, yy[kk] - tt, xo) * a.inv_opt;
+            zv = __builtin_fmaf(2.0f, xv, -xo);
+            xn = __builtin_fmaf(a.rho, xv - xo, xo);
+        }
+        if (TRK) {
+            const float d = xo - xn;
+            const float q = xn + 1e-12f;
+            sd = __builtin_fmaf(d, d, sd);
+            sn = __builtin_fmaf(q, q, sn);
+        }
+        o.z[kk] = zv;
+        o.x2n[kk] = xn;
+    }
+}
+
+template <bool EXACT, bool DN>
+__device__ __forceinline__ void stage_phase_b(const TvArgs& a, const StageRow& ri, const float (&zj)[CPL],
+                                              bool last3, float (&un0)[CPL], float (&un1)[CPL]) {
+    // z of the column right of this lane's last column (lane+1's first)
+    const float zr3 = __int_as_float(
+        __builtin_amdgcn_update_dpp(0, __float_as_int(ri.z[0]), 0x130 /* wave_shl:1 */, 0xF, 0xF, true));
+#pragma unroll
+    for (int kk = 0; kk < CPL; ++kk) {
+        const float zc = ri.z[kk];
+        const float zr = kk < CPL - 1 ? ri.z[kk + 1] : zr3;
+        const float g0 = DN ? ((0.0f - zc) + zj[kk]) : 0.0f;
+        float g1 = (0.0f - zc) + zr;
+        if (kk == CPL - 1) g1 = last3 ? 0.0f : g1;
+        const float uo0 = ri.u0[kk], uo1 = ri.u1[kk];
+        if (EXACT) {
+            const float v0 = uo0 + a.sig_tv * g0;
+            const float v1 = uo1 + a.sig_tv * g1;
+            const float nrm = sqrtf(v0 * v0 + v1 * v1) / a.ths;
+            const float dd = fmaxf(nrm, 1.0f);
+            un0[kk] = uo0 + a.rho * (v0 / dd - uo0);
+            un1[kk] = uo1 + a.rho * (v1 / dd - uo1);
+        } else {
+            const float v0 = __builtin_fmaf(a.sig_tv, g0, uo0);
+            const float v1 = __builtin_fmaf(a.sig_tv, g1, uo1);
+            const float s2 = __builtin_fmaf(v0, v0, v1 * v1);
+            const float f = fminf(1.0f, a.ths * __builtin_amdgcn_rsqf(s2));
+            un0[kk] = __builtin_fmaf(a.rho, __builtin_fmaf(v0, f, -uo0), uo0);
+            un1[kk] = __builtin_fmaf(a.rho, __builtin_fmaf(v1, f, -uo1), uo1);
+        }
+    }
+}
+
+// Stage k's whole life over the plane: steps tbeg (row j = 0: phase A only), then rows
+// j = 1..H-1 (A on j, B on j-1), then j = H (B on H-1 only).  Two row states alternate
+// (RA -> RB -> RA ...) so nothing is copied between steps.
+template <bool EXACT, bool TRK>
+__device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, int k, int nsteps, int lane,
+                                           bool last3, bool core, float& sd, float& sn) {
+    const int H = a.H;
+    const int tbeg = 2 + 2 * k;
+    StageRow RA, RB;
+    float zero[CPL] = {0.f, 0.f, 0.f, 0.f};
+    float lsd = 0.f, lsn = 0.f;
+    int t = 0;
+    for (; t < tbeg; ++t) lds_barrier();
+    // first row (j = 0): phase A only (row above is zero)
+    {
+        const int sl = 0;
+        stage_phase_a<EXACT, TRK>(a, sh.x2[k - 1][sl][lane], sh.u0[k - 1][sl][lane], sh.u1[k - 1][sl][lane],
+                                  sh.y[0][lane], zero, RA, lsd, lsn);
+        lds_barrier();
+        ++t;
+    }
+    auto middle = [&](int j, StageRow& prev, StageRow& cur) {
+        const int sl = j & 1;
+        stage_phase_a<EXACT, TRK>(a, sh.x2[k - 1][sl][lane], sh.u0[k - 1][sl][lane], sh.u1[k - 1][sl][lane],
+                                  sh.y[j & (SP_YRING - 1)][lane], prev.u0, cur, lsd, lsn);
+        float un0[CPL], un1[CPL];
+        stage_phase_b<EXACT, true>(a, prev, cur.z, last3, un0, un1);
+        const int so = (j - 1) & 1;
+        sh.x2[k][so][lane] = make_float4(prev.x2n[0], prev.x2n[1], prev.x2n[2], prev.x2n[3]);
+        sh.u0[k][so][lane] = make_float4(un0[0], un0[1], un0[2], un0[3]);
+        sh.u1[k][so][lane] = make_float4(un1[0], un1[1], un1[2], un1[3]);
+        lds_barrier();
+    };
+    int j = 1;
+    for (; j + 1 < H; j += 2) {
+        middle(j, RA, RB);
+        middle(j + 1, RB, RA);
+    }
+    t += j - 1;
+    StageRow* last = &RA;
+    if (j < H) {
+        middle(j, RA, RB);
+        last = &RB;
+        ++j;
+        ++t;
+    }
+    // last row (i = H-1): phase B only, no forward difference down
+    {
+        float un0[CPL], un1[CPL];
+        stage_phase_b<EXACT, false>(a, *last, zero, last3, un0, un1);
+        const int so = (H - 1) & 1;
+        sh.x2[k][so][lane] = make_float4(last->x2n[0], last->x2n[1], last->x2n[2], last->x2n[3]);
+        sh.u0[k][so][lane] = make_float4(un0[0], un0[1], un0[2], un0[3]);
+        sh.u1[k][so][lane] = make_float4(un1[0], un1[1], un1[2], un1[3]);
+        lds_barrier();
+        ++t;
+    }
+    for (; t < nsteps; ++t) lds_barrier();
+    if (core) { sd += lsd; sn += lsn; }
+}
+
 template <bool EXACT, bool ALPHA1>
 __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     __shared__ StreamShared sh;
     const int lane = threadIdx.x & (WAVE - 1);
-    const int w = threadIdx.x >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (scalar branches)
     const int n = a.n_tv;
     const int H = a.H, W = a.W, C = a.C;
     const long long step = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
@@ -584,12 +746,6 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     const size_t BE = (size_t)a.B * E;
     const size_t plane_off = (size_t)b * E + (size_t)c * HW;
     const int par_in = (int)(step & 1), par_out = (int)((step + 1) & 1);
-    bool hasLeft[CPL], hasRight[CPL];
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) {
-        hasLeft[k] = gj0 + k > 0;
-        hasRight[k] = gj0 + k < W - 1;
-    }
     const int nsteps = H + 4 + 2 * n;
     const int role = (w < SP_FRONT) ? 0 : (w < SP_FRONT + n ? 1 : 2);
     const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -602,27 +758,25 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     if (role == 0) {
         // ---------------- FRONT state ----------------
         const int fw = w;                                  // front wave id (rows r % 4 == fw)
-        float4 fX = zero4, fU0 = zero4, fU1 = zero4, fXS = zero4, fYo = zero4;
-        uchar4 fM = make_uchar4(0, 0, 0, 0);
         uint32_t ph0 = 0, ph1 = 0, ph2 = 0, ph3 = 0;
         float zn0 = 0.f, zn1 = 0.f, zn2 = 0.f, zn3 = 0.f;
         const float* xin = a.x[par_in];
         const float* u2in = a.u2[par_in];
         const float* x2in = ALPHA1 ? nullptr : a.x2[par_in];
+        // The loads of a row are LDS-DMA'd 4 steps before the row is consumed (double-buffered
+        // per front wave), row and column clamped into the plane so every lane loads.
+        const int gjc = min(gj0, W - CPL);
         auto front_issue = [&](int r) {
-            if (r < H && lane_ok) {
-                const size_t base = plane_off + (size_t)r * W + gj0;
-                fX = ld4(xin + base);
-                fYo = ld4(a.yobs + (size_t)b * a.y_cs + (size_t)c * HW + (size_t)r * W + gj0);
-                fM = *reinterpret_cast<const uchar4*>(a.mask + (size_t)b * a.m_cs + (size_t)r * W + gj0);
-                if (!fresh) {
-                    fU0 = ld4(u2in + 2 * base);
-                    fU1 = ld4(u2in + 2 * base + 4);
-                    if (!ALPHA1) fXS = ld4(x2in + base);
-                }
-            }
+            const int rc = min(r, H - 1);
+            const int bi = (r >> 2) & 1;
+            const size_t base = plane_off + (size_t)rc * W + gjc;
+            glds16(xin + base, &sh.fst[fw][bi][0][0]);
+            glds16(a.yobs + (size_t)b * a.y_cs + (size_t)c * HW + (size_t)rc * W + gjc, &sh.fst[fw][bi][1][0]);
+            glds16(u2in + 2 * base, &sh.fst[fw][bi][2][0]);
+            glds16(u2in + 2 * base + 4, &sh.fst[fw][bi][3][0]);
+            if (!ALPHA1) glds16(x2in + base, &sh.fst[fw][bi][4][0]);
+            glds4(a.mask + (size_t)b * a.m_cs + (size_t)rc * W + gjc, &sh.fmk[fw][bi][0]);
         };
-
         front_issue(fw);
         for (int t = 0; t < nsteps; ++t) {
                 // ======================= FRONT =======================
@@ -640,9 +794,18 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
                     } else if (p == 2) {
                         box_muller(ph2, ph3, zn2, zn3);
                     } else {
+                        wait_vm0();   // this wave's DMA of row r (issued 4 steps ago)
+                        const int bi = (r >> 2) & 1;
+                        const float4 fX = sh.fst[fw][bi][0][lane];
+                        const float4 fYo = sh.fst[fw][bi][1][lane];
+                        const float4 fU0 = sh.fst[fw][bi][2][lane];
+                        const float4 fU1 = sh.fst[fw][bi][3][lane];
+                        const float4 fXS = ALPHA1 ? zero4 : sh.fst[fw][bi][4][lane];
+                        const uint32_t fMw = sh.fmk[fw][bi][lane];
                         const float X[CPL] = {fX.x, fX.y, fX.z, fX.w};
                         const float yo[CPL] = {fYo.x, fYo.y, fYo.z, fYo.w};
-                        const float mk[CPL] = {(float)fM.x, (float)fM.y, (float)fM.z, (float)fM.w};
+                        const float mk[CPL] = {(float)(fMw & 0xFFu), (float)((fMw >> 8) & 0xFFu),
+                                               (float)((fMw >> 16) & 0xFFu), (float)(fMw >> 24)};
                         const float Z[CPL] = {zn0, zn1, zn2, zn3};
                         float Yv[CPL];
 #pragma unroll
@@ -660,121 +823,39 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
                         sh.u0[0][s0][lane] = fresh ? zero4 : make_float4(fU0.x, fU0.z, fU1.x, fU1.z);
                         sh.u1[0][s0][lane] = fresh ? zero4 : make_float4(fU0.y, fU0.w, fU1.y, fU1.w);
                         sh.y[r & (SP_YRING - 1)][lane] = Y4;
+                        // keep the ring writes ahead of the DMA issue: an LDS access behind a
+                        // pending LDS-DMA makes the compiler wait vmcnt(0)
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                         front_issue(r + 4);
                     }
                 }
-            __syncthreads();
+            lds_barrier();
         }
     } else if (role == 1) {
-        // ---------------- STAGE state ----------------
-        float pu0[CPL], pu1[CPL], zi[CPL], x2i[CPL];
-#pragma unroll
-        for (int k = 0; k < CPL; ++k) { pu0[k] = 0.f; pu1[k] = 0.f; zi[k] = 0.f; x2i[k] = 0.f; }
-
-        for (int t = 0; t < nsteps; ++t) {
-                // ======================= STAGE k =======================
-                const int k = k_st;
-                const int j = t - 2 - 2 * k;
-                const int i = j - 1;
-                const bool jv = j >= 0 && j < H;
-                const bool iv = i >= 0 && i < H;
-                float zj[CPL], x2nj[CPL], u0o[CPL], u1o[CPL];
-                if (jv) {
-                    const int sl = j & 1;
-                    const float4 X2 = sh.x2[k - 1][sl][lane];
-                    const float4 U0 = sh.u0[k - 1][sl][lane];
-                    const float4 U1 = sh.u1[k - 1][sl][lane];
-                    const float4 YY = sh.y[j & (SP_YRING - 1)][lane];
-                    const float x2o[CPL] = {X2.x, X2.y, X2.z, X2.w};
-                    u0o[0] = U0.x; u0o[1] = U0.y; u0o[2] = U0.z; u0o[3] = U0.w;
-                    u1o[0] = U1.x; u1o[1] = U1.y; u1o[2] = U1.z; u1o[3] = U1.w;
-                    const float yy[CPL] = {YY.x, YY.y, YY.z, YY.w};
-                    const float u1l = __shfl_up(u1o[CPL - 1], 1);
-                    const bool dn = j < H - 1, upv = j > 0;
-#pragma unroll
-                    for (int kk = 0; kk < CPL; ++kk) {
-                        const float u1left = kk > 0 ? u1o[kk - 1] : u1l;
-                        float tt = dn ? (0.0f - u0o[kk]) : 0.0f;
-                        tt = upv ? tt + pu0[kk] : tt;
-                        tt = hasRight[kk] ? tt - u1o[kk] : tt;
-                        tt = hasLeft[kk] ? tt + u1left : tt;
-                        const float xo = x2o[kk];
-                        float xv, zv, xn;
-                        if (EXACT) {
-                            xv = ((xo - a.tau * tt) + a.tau * yy[kk]) / a.opt;
-                            zv = 2.0f * xv - xo;
-                            xn = xo + a.rho * (xv - xo);
-                        } else {
-                            xv = __builtin_fmaf(a.tau, yy[kk] - tt, xo) * a.inv_opt;
-                            zv = __builtin_fmaf(2.0f, xv, -xo);
-                            xn = __builtin_fmaf(a.rho, xv - xo, xo);
-                        }
-                        if (trk && core) {
-                            const float d = xo - xn;
-                            const float q = xn + 1e-12f;
-                            sd += d * d;
-                            sn += q * q;
-                        }
-                        zj[kk] = zv;
-                        x2nj[kk] = xn;
-                    }
-                }
-                if (iv) {
-                    const float zr3 = __shfl_down(zi[0], 1);
-                    const bool dn = i < H - 1;
-                    float un0[CPL], un1[CPL];
-#pragma unroll
-                    for (int kk = 0; kk < CPL; ++kk) {
-                        const float zc = zi[kk];
-                        const float zd = jv ? zj[kk] : 0.f;
-                        const float zr = kk < CPL - 1 ? zi[kk + 1] : zr3;
-                        const float g0 = dn ? ((0.0f - zc) + zd) : 0.0f;
-                        const float g1 = hasRight[kk] ? ((0.0f - zc) + zr) : 0.0f;
-                        const float uo0 = pu0[kk], uo1 = pu1[kk];
-                        if (EXACT) {
-                            const float v0 = uo0 + a.sig_tv * g0;
-                            const float v1 = uo1 + a.sig_tv * g1;
-                            const float nrm = sqrtf(v0 * v0 + v1 * v1) / a.ths;
-                            const float dd = fmaxf(nrm, 1.0f);
-                            un0[kk] = uo0 + a.rho * (v0 / dd - uo0);
-                            un1[kk] = uo1 + a.rho * (v1 / dd - uo1);
-                        } else {
-                            const float v0 = __builtin_fmaf(a.sig_tv, g0, uo0);
-                            const float v1 = __builtin_fmaf(a.sig_tv, g1, uo1);
-                            const float s2 = __builtin_fmaf(v0, v0, v1 * v1);
-                            const float f = fminf(1.0f, a.ths * __builtin_amdgcn_rsqf(s2));
-                            un0[kk] = __builtin_fmaf(a.rho, __builtin_fmaf(v0, f, -uo0), uo0);
-                            un1[kk] = __builtin_fmaf(a.rho, __builtin_fmaf(v1, f, -uo1), uo1);
-                        }
-                    }
-                    const int so = i & 1;
-                    sh.x2[k][so][lane] = make_float4(x2i[0], x2i[1], x2i[2], x2i[3]);
-                    sh.u0[k][so][lane] = make_float4(un0[0], un0[1], un0[2], un0[3]);
-                    sh.u1[k][so][lane] = make_float4(un1[0], un1[1], un1[2], un1[3]);
-                }
-                if (jv) {
-#pragma unroll
-                    for (int kk = 0; kk < CPL; ++kk) {
-                        pu0[kk] = u0o[kk]; pu1[kk] = u1o[kk]; zi[kk] = zj[kk]; x2i[kk] = x2nj[kk];
-                    }
-                }
-            __syncthreads();
-        }
+        // ---------------- STAGE (one inner TV iteration per wave) ----------------
+        // the only column whose forward difference is forced to 0 is the image's right edge;
+        // the left edge, the last row of u2[...,0] and the last column of u2[...,1] need no
+        // select: the DPP shift feeds 0 at lane 0 and TV keeps those dual components exactly 0.
+        const bool last3 = gj0 + CPL - 1 == W - 1;
+        if (trk) stage_loop<EXACT, true>(a, sh, k_st, nsteps, lane, last3, core, sd, sn);
+        else stage_loop<EXACT, false>(a, sh, k_st, nsteps, lane, last3, core, sd, sn);
     } else {
         // ---------------- BACK state ----------------
         const int bw = w - SP_FRONT - n;                   // back wave id (rows r % 2 == bw)
         const StepInfo si = step_info(a, step, a.mean[par_out]);
-        float4 bm = zero4, bq = zero4;
         const float* mean_in = a.mean[par_in];
         const float* sq_in = a.sq[par_in];
+        const bool need_prev = si.acc && !si.first;
+        const int gjc = min(gj0, W - CPL);
         auto back_issue = [&](int r) {
-            if (r < H && core && si.acc && !si.first) {
-                const size_t base = plane_off + (size_t)r * W + gj0;
-                bm = ld4(mean_in + base);
-                bq = ld4(sq_in + base);
+            if (need_prev) {
+                const int rc = min(r, H - 1);
+                const int bi = (r >> 1) & 1;
+                const size_t base = plane_off + (size_t)rc * W + gjc;
+                glds16(mean_in + base, &sh.bst[bw][bi][0][0]);
+                glds16(sq_in + base, &sh.bst[bw][bi][1][0]);
             }
         };
-
         back_issue(bw);
         for (int t = 0; t < nsteps; ++t) {
                 // ======================= BACK =======================
@@ -800,6 +881,12 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
                         *reinterpret_cast<float4*>(u2o + 4) = make_float4(U0.z, U1.z, U0.w, U1.w);
                         if (!ALPHA1) *reinterpret_cast<float4*>(a.x2[par_out] + base) = X2;
                         if (si.acc) {
+                            float4 bm = zero4, bq = zero4;
+                            if (need_prev) {
+                                wait_vm0();
+                                bm = sh.bst[bw][(r >> 1) & 1][0][lane];
+                                bq = sh.bst[bw][(r >> 1) & 1][1][lane];
+                            }
                             const float xs[CPL] = {Xo.x, Xo.y, Xo.z, Xo.w};
                             const float ms[CPL] = {bm.x, bm.y, bm.z, bm.w};
                             const float qs[CPL] = {bq.x, bq.y, bq.z, bq.w};
@@ -826,9 +913,10 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
                         }
                         if (si.sample) *reinterpret_cast<float4*>(a.samples + (size_t)si.sidx * BE + base) = Xo;
                     }
+                    asm volatile("" ::: "memory");
                     back_issue(r + 2);
                 }
-            __syncthreads();
+            lds_barrier();
         }
     }
 
@@ -838,7 +926,7 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
         sn = wave_sum(sn);
         if (lane == 0) { sh.red[k_st - 1][0] = sd; sh.red[k_st - 1][1] = sn; }
     }
-    __syncthreads();
+    lds_barrier();
     if (threadIdx.x >= 2 && (int)threadIdx.x <= n - 2) {
         const int tt = threadIdx.x;
         const int g = a.per_chain_norm ? b : 0;
