@@ -40,7 +40,7 @@ def build_native(force: bool = False, verbose: bool = False, out: str = OUT) -> 
     if not force and out == OUT and up_to_date():
         return OUT
     extra = os.environ.get("PSGLA_HIPCC_EXTRA", "").split()
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-fPIC",
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-Wno-inline-asm", "-fPIC",
            "-shared", "-I", os.path.join(REPO, "include"), "-o", out + ".tmp"] + extra + SOURCES
     if verbose:
         print(" ".join(cmd))

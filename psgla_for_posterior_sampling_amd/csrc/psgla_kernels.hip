@@ -85,6 +85,7 @@ struct TvArgs {
     // tiling
     int nbands, band_h, nsegs, seg_w, tiles, halo;
     int stream;                     // 1: main pass = row-streaming pipeline kernel
+    unsigned long long* stamps;     // diagnostic build only (PSGLA_STAMPS): per-wave work/wait cycles
 };
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -548,18 +549,68 @@ typedef __attribute__((address_space(1))) const void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
 
 // 16 B (4 B) per lane from global memory straight into LDS; lane i lands at dst + 16 i (4 i).
+// Issued as inline asm: the compiler does not track these loads, so it cannot insert a
+// conservative vmcnt(0) before unrelated LDS accesses -- the waves wait with counted
+// s_waitcnt vmcnt(N) themselves (vector-memory operations retire in issue order).
 __device__ __forceinline__ void glds16(const void* src, void* dst) {
-    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+    const unsigned off = (unsigned)(size_t)(lptr_t)dst;
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :: "v"(src), "s"(off) : "memory", "m0");
 }
 __device__ __forceinline__ void glds4(const void* src, void* dst) {
-    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 4, 0, 0);
+    const unsigned off = (unsigned)(size_t)(lptr_t)dst;
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off"
+                 :: "v"(src), "s"(off) : "memory", "m0");
 }
 // Workgroup barrier that only drains LDS (lgkmcnt): LDS-DMA loads stay in flight across it
 // (a __syncthreads() fence would wait vmcnt(0) while a global_load_lds is pending).
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
-__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+template <int N>
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory"); }
+__device__ __forceinline__ void wait_vm0() { wait_vm<0>(); }
+// vmcnt(n) for a wave-uniform n in [0, 8]
+__device__ __forceinline__ void wait_vm_n(int n) {
+    switch (n) {
+        case 0: wait_vm<0>(); break;
+        case 1: wait_vm<1>(); break;
+        case 2: wait_vm<2>(); break;
+        case 3: wait_vm<3>(); break;
+        case 4: wait_vm<4>(); break;
+        case 5: wait_vm<5>(); break;
+        case 6: wait_vm<6>(); break;
+        case 7: wait_vm<7>(); break;
+        default: wait_vm<8>(); break;
+    }
+}
+
+// Diagnostic build (-DPSGLA_STAMPS): every wave accumulates the cycles it spends working
+// between two pipeline barriers and the cycles it waits at them (s_memtime, shader clock).
+struct Stamps {
+    unsigned long long work = 0, wait = 0, t0 = 0;
+};
+__device__ __forceinline__ unsigned long long stamp_now() {
+#ifdef PSGLA_STAMPS
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    return t;
+#else
+    return 0;
+#endif
+}
+__device__ __forceinline__ void step_barrier(Stamps& st) {
+#ifdef PSGLA_STAMPS
+    const unsigned long long t1 = stamp_now();
+    st.work += t1 - st.t0;
+    lds_barrier();
+    st.t0 = stamp_now();
+    st.wait += st.t0 - t1;
+#else
+    (void)st;
+    lds_barrier();
+#endif
+}
 
 struct StepInfo {
     bool acc, first, blockend, liveout, sample;
@@ -663,64 +714,88 @@ __device__ __forceinline__ void stage_phase_b(const TvArgs& a, const StageRow& r
     }
 }
 
-// Stage k's whole life over the plane: steps tbeg (row j = 0: phase A only), then rows
-// j = 1..H-1 (A on j, B on j-1), then j = H (B on H-1 only).  Two row states alternate
-// (RA -> RB -> RA ...) so nothing is copied between steps.
+// Stage k's whole life over the plane.  At step t the stage (lookahead row j = t - 3k - 1)
+//   1. issues the LDS reads of ring k-1 row j,
+//   2. runs the dual update of row i = j - 2 -- every input is already in registers (z of
+//      rows i and i+1 from the two previous steps) -- and writes row i to ring k,
+//   3. runs the primal update of row j once the reads have landed.
+// The ring reads' latency and the ring writes thus overlap computation instead of
+// bracketing it.  Three row states rotate (RA -> RB -> RC) so nothing is copied.
 template <bool EXACT, bool TRK>
 __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, int k, int nsteps, int lane,
-                                           bool last3, bool core, float& sd, float& sn) {
+                                           bool last3, bool core, float& sd, float& sn, Stamps& stp) {
     const int H = a.H;
-    const int tbeg = 2 + 2 * k;
-    StageRow RA, RB;
-    float zero[CPL] = {0.f, 0.f, 0.f, 0.f};
+    const int tbeg = 1 + 3 * k;          // step of lookahead row 0
+    StageRow RA, RB, RC;
+    const float zero[CPL] = {0.f, 0.f, 0.f, 0.f};
     float lsd = 0.f, lsn = 0.f;
     int t = 0;
-    for (; t < tbeg; ++t) lds_barrier();
-    // first row (j = 0): phase A only (row above is zero)
-    {
-        const int sl = 0;
-        stage_phase_a<EXACT, TRK>(a, sh.x2[k - 1][sl][lane], sh.u0[k - 1][sl][lane], sh.u1[k - 1][sl][lane],
-                                  sh.y[0][lane], zero, RA, lsd, lsn);
-        lds_barrier();
-        ++t;
-    }
-    auto middle = [&](int j, StageRow& prev, StageRow& cur) {
+    for (; t < tbeg; ++t) step_barrier(stp);
+    auto load_row = [&](int j, float4& X2, float4& U0, float4& U1, float4& YY) {
         const int sl = j & 1;
-        stage_phase_a<EXACT, TRK>(a, sh.x2[k - 1][sl][lane], sh.u0[k - 1][sl][lane], sh.u1[k - 1][sl][lane],
-                                  sh.y[j & (SP_YRING - 1)][lane], prev.u0, cur, lsd, lsn);
-        float un0[CPL], un1[CPL];
-        stage_phase_b<EXACT, true>(a, prev, cur.z, last3, un0, un1);
-        const int so = (j - 1) & 1;
-        sh.x2[k][so][lane] = make_float4(prev.x2n[0], prev.x2n[1], prev.x2n[2], prev.x2n[3]);
-        sh.u0[k][so][lane] = make_float4(un0[0], un0[1], un0[2], un0[3]);
-        sh.u1[k][so][lane] = make_float4(un1[0], un1[1], un1[2], un1[3]);
-        lds_barrier();
+        X2 = sh.x2[k - 1][sl][lane];
+        U0 = sh.u0[k - 1][sl][lane];
+        U1 = sh.u1[k - 1][sl][lane];
+        YY = sh.y[j & (SP_YRING - 1)][lane];
     };
-    int j = 1;
-    for (; j + 1 < H; j += 2) {
-        middle(j, RA, RB);
-        middle(j + 1, RB, RA);
-    }
-    t += j - 1;
-    StageRow* last = &RA;
-    if (j < H) {
-        middle(j, RA, RB);
-        last = &RB;
-        ++j;
-        ++t;
-    }
-    // last row (i = H-1): phase B only, no forward difference down
-    {
-        float un0[CPL], un1[CPL];
-        stage_phase_b<EXACT, false>(a, *last, zero, last3, un0, un1);
-        const int so = (H - 1) & 1;
-        sh.x2[k][so][lane] = make_float4(last->x2n[0], last->x2n[1], last->x2n[2], last->x2n[3]);
+    auto store_row = [&](int i, const StageRow& r, const float (&un0)[CPL], const float (&un1)[CPL]) {
+        const int so = i & 1;
+        sh.x2[k][so][lane] = make_float4(r.x2n[0], r.x2n[1], r.x2n[2], r.x2n[3]);
         sh.u0[k][so][lane] = make_float4(un0[0], un0[1], un0[2], un0[3]);
         sh.u1[k][so][lane] = make_float4(un1[0], un1[1], un1[2], un1[3]);
-        lds_barrier();
-        ++t;
+    };
+    // rows 0 and 1: primal update only
+    {
+        float4 X2, U0, U1, YY;
+        load_row(0, X2, U0, U1, YY);
+        stage_phase_a<EXACT, TRK>(a, X2, U0, U1, YY, zero, RA, lsd, lsn);
+        step_barrier(stp);
+        load_row(1, X2, U0, U1, YY);
+        stage_phase_a<EXACT, TRK>(a, X2, U0, U1, YY, RA.u0, RB, lsd, lsn);
+        step_barrier(stp);
+        t += 2;
     }
-    for (; t < nsteps; ++t) lds_barrier();
+    // middle rows j = 2..H-1: dual update of row j-2 (p2) with z of row j-1 (p1), then primal of j
+    auto middle = [&](int j, StageRow& p2, StageRow& p1, StageRow& cur) {
+        float4 X2, U0, U1, YY;
+        load_row(j, X2, U0, U1, YY);
+        float un0[CPL], un1[CPL];
+        stage_phase_b<EXACT, true>(a, p2, p1.z, last3, un0, un1);
+        store_row(j - 2, p2, un0, un1);
+        stage_phase_a<EXACT, TRK>(a, X2, U0, U1, YY, p1.u0, cur, lsd, lsn);
+        step_barrier(stp);
+    };
+    int j = 2;
+    for (; j + 2 < H; j += 3) {
+        middle(j, RA, RB, RC);
+        middle(j + 1, RB, RC, RA);
+        middle(j + 2, RC, RA, RB);
+    }
+    t += (j - 2);
+    // j = H: dual update of row H-2 (z of row H-1 known); j = H+1: row H-1 (no row below).
+    // (static buffer roles per remainder: a runtime-indexed StageRow would go to scratch)
+    auto finish = [&](StageRow& r2, StageRow& r1) {
+        float un0[CPL], un1[CPL];
+        stage_phase_b<EXACT, true>(a, r2, r1.z, last3, un0, un1);
+        store_row(H - 2, r2, un0, un1);
+        step_barrier(stp);
+        stage_phase_b<EXACT, false>(a, r1, zero, last3, un0, un1);
+        store_row(H - 1, r1, un0, un1);
+        step_barrier(stp);
+    };
+    const int rem = H - j;              // 0, 1 or 2 middle rows left
+    if (rem == 0) {
+        finish(RA, RB);
+    } else if (rem == 1) {
+        middle(j, RA, RB, RC);
+        finish(RB, RC);
+    } else {
+        middle(j, RA, RB, RC);
+        middle(j + 1, RB, RC, RA);
+        finish(RC, RA);
+    }
+    t += rem + 2;
+    for (; t < nsteps; ++t) step_barrier(stp);
     if (core) { sd += lsd; sn += lsn; }
 }
 
@@ -746,9 +821,11 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     const size_t BE = (size_t)a.B * E;
     const size_t plane_off = (size_t)b * E + (size_t)c * HW;
     const int par_in = (int)(step & 1), par_out = (int)((step + 1) & 1);
-    const int nsteps = H + 4 + 2 * n;
+    const int nsteps = H + 4 + 3 * n;
     const int role = (w < SP_FRONT) ? 0 : (w < SP_FRONT + n ? 1 : 2);
     const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    Stamps stp;
+    stp.t0 = stamp_now();
 
     float sd = 0.f, sn = 0.f;
     const int k_st = w - SP_FRONT + 1;                 // inner TV iteration (1-based)
@@ -829,7 +906,7 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
                         front_issue(r + 4);
                     }
                 }
-            lds_barrier();
+            step_barrier(stp);
         }
     } else if (role == 1) {
         // ---------------- STAGE (one inner TV iteration per wave) ----------------
@@ -837,8 +914,8 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
         // the left edge, the last row of u2[...,0] and the last column of u2[...,1] need no
         // select: the DPP shift feeds 0 at lane 0 and TV keeps those dual components exactly 0.
         const bool last3 = gj0 + CPL - 1 == W - 1;
-        if (trk) stage_loop<EXACT, true>(a, sh, k_st, nsteps, lane, last3, core, sd, sn);
-        else stage_loop<EXACT, false>(a, sh, k_st, nsteps, lane, last3, core, sd, sn);
+        if (trk) stage_loop<EXACT, true>(a, sh, k_st, nsteps, lane, last3, core, sd, sn, stp);
+        else stage_loop<EXACT, false>(a, sh, k_st, nsteps, lane, last3, core, sd, sn, stp);
     } else {
         // ---------------- BACK state ----------------
         const int bw = w - SP_FRONT - n;                   // back wave id (rows r % 2 == bw)
@@ -856,10 +933,12 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
                 glds16(sq_in + base, &sh.bst[bw][bi][1][0]);
             }
         };
+        // vector-memory stores per row (all lanes of a wave store together; lane 0 is core)
+        const int nst = 3 + (ALPHA1 ? 0 : 1) + ((si.acc && (si.blockend || si.liveout)) ? 2 : 0) + (si.sample ? 1 : 0);
         back_issue(bw);
         for (int t = 0; t < nsteps; ++t) {
                 // ======================= BACK =======================
-                const int r = t - 4 - 2 * n;
+                const int r = t - 4 - 3 * n;
                 if (r >= 0 && r < H && (r & 1) == bw) {
                     const int sl = r & 1;
                     const float4 X2 = sh.x2[n][sl][lane];
@@ -873,6 +952,37 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
                         Xo.z = (1.0f - a.alpha) * YY.z + a.alpha * X2.z;
                         Xo.w = (1.0f - a.alpha) * YY.w + a.alpha * X2.w;
                     }
+                    float4 M4 = zero4, Q4 = zero4;
+                    if (si.acc) {
+                        float4 bm = zero4, bq = zero4;
+                        if (need_prev) {
+                            // DMA of row r was issued just before the previous row's nst stores
+                            wait_vm_n(r == bw ? 0 : nst);
+                            bm = sh.bst[bw][(r >> 1) & 1][0][lane];
+                            bq = sh.bst[bw][(r >> 1) & 1][1][lane];
+                        }
+                        const float xs[CPL] = {Xo.x, Xo.y, Xo.z, Xo.w};
+                        const float ms[CPL] = {bm.x, bm.y, bm.z, bm.w};
+                        const float qs[CPL] = {bq.x, bq.y, bq.z, bq.w};
+                        float m[CPL], q[CPL];
+#pragma unroll
+                        for (int kk = 0; kk < CPL; ++kk) {
+                            if (si.first) {
+                                m[kk] = si.cb * xs[kk];
+                                q[kk] = si.cb * (xs[kk] * xs[kk]);
+                            } else {
+                                m[kk] = si.ca * ms[kk] + si.cb * xs[kk];
+                                q[kk] = si.ca * qs[kk] + si.cb * (xs[kk] * xs[kk]);
+                            }
+                        }
+                        M4 = make_float4(m[0], m[1], m[2], m[3]);
+                        Q4 = make_float4(q[0], q[1], q[2], q[3]);
+                    }
+                    // all LDS reads of this row (ring + staging) done before the staging
+                    // buffer is re-targeted by the next DMA
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    back_issue(r + 2);
+                    asm volatile("" ::: "memory");
                     if (core) {
                         const size_t base = plane_off + (size_t)r * W + gj0;
                         *reinterpret_cast<float4*>(a.x[par_out] + base) = Xo;
@@ -881,28 +991,6 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
                         *reinterpret_cast<float4*>(u2o + 4) = make_float4(U0.z, U1.z, U0.w, U1.w);
                         if (!ALPHA1) *reinterpret_cast<float4*>(a.x2[par_out] + base) = X2;
                         if (si.acc) {
-                            float4 bm = zero4, bq = zero4;
-                            if (need_prev) {
-                                wait_vm0();
-                                bm = sh.bst[bw][(r >> 1) & 1][0][lane];
-                                bq = sh.bst[bw][(r >> 1) & 1][1][lane];
-                            }
-                            const float xs[CPL] = {Xo.x, Xo.y, Xo.z, Xo.w};
-                            const float ms[CPL] = {bm.x, bm.y, bm.z, bm.w};
-                            const float qs[CPL] = {bq.x, bq.y, bq.z, bq.w};
-                            float m[CPL], q[CPL];
-#pragma unroll
-                            for (int kk = 0; kk < CPL; ++kk) {
-                                if (si.first) {
-                                    m[kk] = si.cb * xs[kk];
-                                    q[kk] = si.cb * (xs[kk] * xs[kk]);
-                                } else {
-                                    m[kk] = si.ca * ms[kk] + si.cb * xs[kk];
-                                    q[kk] = si.ca * qs[kk] + si.cb * (xs[kk] * xs[kk]);
-                                }
-                            }
-                            const float4 M4 = make_float4(m[0], m[1], m[2], m[3]);
-                            const float4 Q4 = make_float4(q[0], q[1], q[2], q[3]);
                             if (si.blockend) {
                                 *reinterpret_cast<float4*>(a.blocks + (size_t)si.blk * BE + base) = M4;
                                 *reinterpret_cast<float4*>(a.blocks2 + (size_t)si.blk * BE + base) = Q4;
@@ -913,13 +1001,17 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
                         }
                         if (si.sample) *reinterpret_cast<float4*>(a.samples + (size_t)si.sidx * BE + base) = Xo;
                     }
-                    asm volatile("" ::: "memory");
-                    back_issue(r + 2);
                 }
-            lds_barrier();
+            step_barrier(stp);
         }
     }
 
+#ifdef PSGLA_STAMPS
+    if (a.stamps && lane == 0) {
+        a.stamps[((size_t)blockIdx.x * 16 + w) * 2] = stp.work;
+        a.stamps[((size_t)blockIdx.x * 16 + w) * 2 + 1] = stp.wait;
+    }
+#endif
     // rel_err partial sums of this plane -> global (deepinv's early-stop test, per chain)
     if (role == 1 && trk) {
         sd = wave_sum(sd);
@@ -1216,6 +1308,7 @@ int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream) {
     a.d_step = (long long*)s->d_step; a.step_offset = s->step_offset;
     a.fresh_dev = d->fresh; a.per_chain_norm = 1; a.norms = d->norms; a.arrive = d->arrive;
     a.advance_step = d->advance_step;
+    a.stamps = (unsigned long long*)d->debug_stamps;
     a.n_inter = s->n_inter; a.nm = s->n_inter_mmse; a.coef = s->acc_coef;
     a.samples = s->samples; a.samples_cap = s->samples_cap;
     a.blocks = s->blocks; a.blocks2 = s->blocks2; a.blocks_cap = s->blocks_cap;
