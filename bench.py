@@ -49,6 +49,7 @@ def parse():
     p.add_argument("--graph-steps", type=int, default=20)
     p.add_argument("--exact", action="store_true", help="bit-exact (IEEE div/sqrt) TV kernel")
     p.add_argument("--kernel-iters", type=int, default=50)
+    p.add_argument("--tv-iters", type=int, default=10, help="TV n_it_max (analysis only; the workload is 10)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r01_pmc_tv_main.json"))
@@ -143,7 +144,7 @@ def main():
     n_iter = args.warmup + args.steps
     eng = FusedTvChains(init.contiguous(), y.contiguous(), mask_2d.to(torch.uint8), c1=c1f, c2=c2f,
                         sigma2=float(np.float32(sigma1 ** 2)), alpha=1.0, ths=float(np.float32(s)),
-                        tv=K.TvConstants(n_it_max=10), seed=0, n_iter=n_iter + args.kernel_iters,
+                        tv=K.TvConstants(n_it_max=args.tv_iters), seed=0, n_iter=n_iter + args.kernel_iters,
                         n_inter=n_inter, n_inter_mmse=nm, chain0=c0, exact=args.exact)
     gs = max(1, min(args.graph_steps, args.steps))
     # warm-up: eager steps + graph capture

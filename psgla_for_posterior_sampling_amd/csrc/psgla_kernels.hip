@@ -570,26 +570,33 @@ __device__ __forceinline__ void lds_barrier() {
 template <int N>
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory"); }
 __device__ __forceinline__ void wait_vm0() { wait_vm<0>(); }
-// vmcnt(n) for a wave-uniform n in [0, 8]
-__device__ __forceinline__ void wait_vm_n(int n) {
-    switch (n) {
-        case 0: wait_vm<0>(); break;
-        case 1: wait_vm<1>(); break;
-        case 2: wait_vm<2>(); break;
-        case 3: wait_vm<3>(); break;
-        case 4: wait_vm<4>(); break;
-        case 5: wait_vm<5>(); break;
-        case 6: wait_vm<6>(); break;
-        case 7: wait_vm<7>(); break;
-        default: wait_vm<8>(); break;
+// vmcnt(n) for a wave-uniform n in [0, 23] (larger n waits for 23)
+template <int N>
+__device__ __forceinline__ void wait_vm_le(int n) {
+    if constexpr (N >= 23) {
+        wait_vm<23>();
+    } else {
+        if (n == N) wait_vm<N>();
+        else wait_vm_le<N + 1>(n);
     }
 }
+__device__ __forceinline__ void wait_vm_n(int n) { wait_vm_le<0>(n); }
 
 // Diagnostic build (-DPSGLA_STAMPS): every wave accumulates the cycles it spends working
 // between two pipeline barriers and the cycles it waits at them (s_memtime, shader clock).
 struct Stamps {
     unsigned long long work = 0, wait = 0, t0 = 0;
+    unsigned long long* tr = nullptr;   // per-step arrival / release times (workgroup 0 only)
+    int t = 0, w = 0;
+    unsigned long long seg[4] = {0, 0, 0, 0}, ts = 0;
 };
+#ifdef PSGLA_STAMPS
+#define STAMP_SEG(st, i) do { const unsigned long long _n = stamp_now(); (st).seg[i] += _n - (st).ts; (st).ts = _n; } while (0)
+#define STAMP_START(st) do { (st).ts = stamp_now(); } while (0)
+#else
+#define STAMP_SEG(st, i) do { } while (0)
+#define STAMP_START(st) do { } while (0)
+#endif
 __device__ __forceinline__ unsigned long long stamp_now() {
 #ifdef PSGLA_STAMPS
     unsigned long long t;
@@ -606,6 +613,11 @@ __device__ __forceinline__ void step_barrier(Stamps& st) {
     lds_barrier();
     st.t0 = stamp_now();
     st.wait += st.t0 - t1;
+    if (st.tr && (threadIdx.x & 63) == 0) {
+        st.tr[((size_t)st.t * 16 + st.w) * 2] = t1;
+        st.tr[((size_t)st.t * 16 + st.w) * 2 + 1] = st.t0;
+    }
+    ++st.t;
 #else
     (void)st;
     lds_barrier();
@@ -826,6 +838,10 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
     Stamps stp;
     stp.t0 = stamp_now();
+#ifdef PSGLA_STAMPS
+    stp.w = w;
+    stp.tr = (a.stamps && blockIdx.x == 0) ? a.stamps + (size_t)gridDim.x * 32 : nullptr;
+#endif
 
     float sd = 0.f, sn = 0.f;
     const int k_st = w - SP_FRONT + 1;                 // inner TV iteration (1-based)
@@ -871,7 +887,9 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
                     } else if (p == 2) {
                         box_muller(ph2, ph3, zn2, zn3);
                     } else {
+                        STAMP_START(stp);
                         wait_vm0();   // this wave's DMA of row r (issued 4 steps ago)
+                        STAMP_SEG(stp, 0);
                         const int bi = (r >> 2) & 1;
                         const float4 fX = sh.fst[fw][bi][0][lane];
                         const float4 fYo = sh.fst[fw][bi][1][lane];
@@ -896,14 +914,14 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
                         else x2s = ALPHA1 ? fX : fXS;
                         if (!lane_ok) x2s = zero4;
                         const int s0 = r & 1;
+                        STAMP_SEG(stp, 1);
                         sh.x2[0][s0][lane] = x2s;
                         sh.u0[0][s0][lane] = fresh ? zero4 : make_float4(fU0.x, fU0.z, fU1.x, fU1.z);
                         sh.u1[0][s0][lane] = fresh ? zero4 : make_float4(fU0.y, fU0.w, fU1.y, fU1.w);
                         sh.y[r & (SP_YRING - 1)][lane] = Y4;
-                        // keep the ring writes ahead of the DMA issue: an LDS access behind a
-                        // pending LDS-DMA makes the compiler wait vmcnt(0)
-                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                        front_issue(r + 4);
+                        STAMP_SEG(stp, 2);
+                        front_issue(r + 4);   // into the buffer of row r - 4 (consumed 4 steps ago)
+                        STAMP_SEG(stp, 3);
                     }
                 }
             step_barrier(stp);
@@ -1010,6 +1028,10 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     if (a.stamps && lane == 0) {
         a.stamps[((size_t)blockIdx.x * 16 + w) * 2] = stp.work;
         a.stamps[((size_t)blockIdx.x * 16 + w) * 2 + 1] = stp.wait;
+        if (w < SP_FRONT) {
+            unsigned long long* sg = a.stamps + (size_t)gridDim.x * 32 + (size_t)nsteps * 32 + ((size_t)blockIdx.x * 4 + w) * 4;
+            for (int i = 0; i < 4; ++i) sg[i] = stp.seg[i];
+        }
     }
 #endif
     // rel_err partial sums of this plane -> global (deepinv's early-stop test, per chain)
