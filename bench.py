@@ -16,7 +16,7 @@ all_reduce after the timed region combines the per-chain MMSE PSNR.
 Timed region: K steps replayed from a hipGraph (the device step counter advances the noise
 counter, block-mean coefficients and sample / block slots), barrier + synchronize on both
 sides, max over ranks.  value = chain-steps (image-steps of 3x256x256) per second over all
-GPUs.  The dominant kernel (tv_main_kernel) is also timed alone with HIP events on its own
+GPUs.  The dominant kernel (tv_stream_kernel) is also timed alone with HIP events on its own
 stream for the roofline figure.
 """
 from __future__ import annotations
@@ -52,12 +52,12 @@ def parse():
     p.add_argument("--tv-iters", type=int, default=10, help="TV n_it_max (analysis only; the workload is 10)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r01_pmc_tv_main.json"))
+    p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r01_pmc_tv_stream.json"))
     return p.parse_args()
 
 
 def algorithmic_bytes_per_launch(B, C, H, W, step0, steps, n_inter, nm):
-    """Compulsory HBM bytes of one tv_main_kernel launch, averaged over the timed steps.
+    """Compulsory HBM bytes of one fused-step kernel launch, averaged over the timed steps.
     Per element: read X 4 + u2 8 + y 4 (+ mean 4 + sq 4 unless the block restarts), write
     X 4 + u2 8 + mean 4 + sq 4 (block means instead of the live accumulators at a block
     end), + the sample copy 4 every n_inter steps; + the (H,W) u8 mask once per launch."""
@@ -223,7 +223,7 @@ def main():
                        "batch_steps_per_s_per_gpu": round(steps / dt, 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "tv_main_kernel", "kernel_ms": round(kern_ms, 5),
+                         "kernel": eng.main_kernel, "kernel_ms": round(kern_ms, 5),
                          "algorithmic_bytes_per_launch": int(alg_bytes)},
             "cpu_baseline": cpu,
             "mmse_psnr_mean_db": round(psnr_sum / max(n_chains, 1), 3),

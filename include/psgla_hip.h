@@ -101,8 +101,10 @@ typedef struct PsglaTvStep {
                                  idempotent, for kernel timing); 2: finaliser only            */
     int32_t kernel_variant;   /* 0: auto (row-streaming pipeline when W % 4 == 0 and n_tv <= 10,
                                  else temporally blocked bands); 1: force bands; 2: force stream */
-    uint64_t* debug_stamps;   /* diagnostic builds only (-DPSGLA_STAMPS): [workgroups][16 waves][2]
-                                 work / wait shader cycles of the streaming kernel; else NULL  */
+    uint64_t* debug_stamps;   /* diagnostic builds only (-DPSGLA_STAMPS), else NULL: [workgroups][16][2]
+                                 work / wait shader cycles per wave of the streaming kernel, then
+                                 [steps][16][2] barrier arrival / release times of workgroup 0,
+                                 then [workgroups][4][4] front-wave segment cycles (tools/stamps.py) */
 } PsglaTvStep;
 
 int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream);

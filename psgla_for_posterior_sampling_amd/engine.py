@@ -129,6 +129,14 @@ class FusedTvChains:
             self.graph.replay()
             self.steps_done += self.graph_steps
 
+    @property
+    def main_kernel(self) -> str:
+        """Name of the kernel psgla_tv_step dispatches for this shape (psgla_kernels.hip:
+        streaming when W % 4 == 0, 1 <= n_tv <= 10 and H >= 2, unless the band kernel is forced)."""
+        d = self.desc
+        streamable = d.W % 4 == 0 and 1 <= d.n_tv <= 10 and d.H >= 2
+        return "tv_stream_kernel" if streamable and d.kernel_variant != 1 else "tv_main_kernel"
+
     def launch_main_only(self, n: int = 1):
         """Launch only the fused tile kernel n times for the CURRENT step (idempotent: it reads
         the step's inputs and rewrites the same outputs; the step counter does not move).

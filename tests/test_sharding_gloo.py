@@ -1,0 +1,91 @@
+"""Multi-process sharding of chains (world size 2, gloo on CPU, 127.0.0.1).
+
+The GPU path shards chains contiguously over ranks (sharding.chain_range) and keys each chain's
+noise by its GLOBAL id, so the union of the ranks' chains equals the single-process run; the only
+collectives are the final all_reduce of PSNR sums and all_gather of per-chain images
+(sharding.reduce_psnr / gather_chains).  Each rank here runs the CPU checker
+(oracle.psgla, one chain at a time, as the reference runs one chain per image) on its shard.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from psgla_for_posterior_sampling_amd.sharding import chain_range, gather_chains, psnr, reduce_psnr
+
+
+def test_chain_range_partitions():
+    for total in (0, 1, 5, 64, 65):
+        for world in (1, 2, 3, 8):
+            got = [chain_range(total, world, r) for r in range(world)]
+            assert got[0][0] == 0 and got[-1][1] == total
+            for (a0, a1), (b0, b1) in zip(got, got[1:]):
+                assert a1 == b0
+            sizes = [b - a for a, b in got]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        chain_range(4, 2, 2)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+TOTAL = 5          # uneven split: 3 + 2
+H = W = 8
+N_ITER, N_INTER = 20, 5
+
+
+def _run_chains(c0, c1):
+    """Per-chain oracle runs: ground truth, blocks (nb, B, C, H, W) and last samples."""
+    from oracle import psgla_oracle as orc
+    gts, blocks, lasts = [], [], []
+    for c in range(c0, c1):
+        g = torch.Generator().manual_seed(1234 + c)
+        x = torch.rand((1, 3, H, W), generator=g)
+        dg, y, init, _ = orc.inpainting_problem(x, seed_ip=0)
+        s = 10 / 255.0
+        Xl, M, _ = orc.psgla(init, dg, orc.ClampDenoiser(), torch.tensor(1.0), torch.tensor(10.0), sig_float=s,
+                             delta=s ** 2, n_iter=N_ITER, n_inter=N_INTER, n_inter_mmse=N_INTER - 1, seed=0, chain=c)
+        gts.append(x[0])
+        blocks.append(torch.stack(M))
+        lasts.append(Xl[-1])
+    if not gts:
+        return torch.zeros((0, 3, H, W)), torch.zeros((2, 0, 3, H, W)), torch.zeros((0, 3, H, W))
+    return torch.stack(gts), torch.stack(blocks, dim=1), torch.stack(lasts)
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c0, c1 = chain_range(TOTAL, world, rank)
+        gt, blocks, last = _run_chains(c0, c1)
+        s, n = reduce_psnr(blocks, gt, world)
+        full_last = gather_chains(last, TOTAL, world)
+        full_gt = gather_chains(gt, TOTAL, world)
+        torch.save({"psnr_sum": s, "n": n, "last": full_last, "gt": full_gt}, os.path.join(out_dir, f"r{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_sharding_matches_single_process(tmp_path):
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    gt, blocks, last = _run_chains(0, TOTAL)
+    ref_psnr = psnr(gt, blocks.mean(dim=0)).sum().item()
+    for r in range(world):
+        got = torch.load(os.path.join(tmp_path, f"r{r}.pt"), weights_only=True)
+        assert got["n"] == TOTAL
+        assert abs(got["psnr_sum"] - ref_psnr) < 1e-9 * max(1.0, abs(ref_psnr))
+        assert torch.equal(got["last"], last)        # bit-identical per chain, any split
+        assert torch.equal(got["gt"], gt)
