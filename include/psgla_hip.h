@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PSGLA_HIP_ABI_VERSION 1
+#define PSGLA_HIP_ABI_VERSION 2
 
 /* Max inner TV iterations the fused (temporally blocked) kernel handles. */
 #define PSGLA_TV_MAX_FUSED_IT 24
@@ -105,6 +105,9 @@ typedef struct PsglaTvStep {
                                  work / wait shader cycles per wave of the streaming kernel, then
                                  [steps][16][2] barrier arrival / release times of workgroup 0,
                                  then [workgroups][4][4] front-wave segment cycles (tools/stamps.py) */
+    int32_t stream_wgs;       /* streaming kernel work split: 0 auto (rows of all planes cut into
+                                 one contiguous range per CU, n_tv halo rows at cuts, when W <= 256);
+                                 -1 one workgroup per plane; > 0 force that many row ranges      */
 } PsglaTvStep;
 
 int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream);

@@ -85,6 +85,7 @@ struct TvArgs {
     // tiling
     int nbands, band_h, nsegs, seg_w, tiles, halo;
     int stream;                     // 1: main pass = row-streaming pipeline kernel
+    int split_wgs;                  // stream kernel: > 0 = row-split mode over this many workgroups
     unsigned long long* stamps;     // diagnostic build only (PSGLA_STAMPS): per-wave work/wait cycles
 };
 
@@ -531,6 +532,8 @@ constexpr int SP_FRONT = 4;
 constexpr int SP_BACK = 2;
 constexpr int SP_MAXST = 10;
 constexpr int SP_YRING = 32;
+constexpr int SP_MAXSEG = 4;      // planes touched by one workgroup's row stream (split mode)
+constexpr int SP_NOSEG = 1 << 30; // "no further segment start"
 
 struct StreamShared {
     float4 x2[SP_MAXST + 1][2][WAVE];     // ring k = output of stage k (k = 0: front), 2 row slots
@@ -542,7 +545,7 @@ struct StreamShared {
     float4 fst[SP_FRONT][2][5][WAVE];
     uint32_t fmk[SP_FRONT][2][WAVE];
     float4 bst[SP_BACK][2][2][WAVE];
-    float red[SP_MAXST][2];
+    float red[SP_MAXSEG][SP_MAXST][2];
 };
 
 typedef __attribute__((address_space(1))) const void* gptr_t;
@@ -647,6 +650,94 @@ __device__ __forceinline__ StepInfo step_info(const TvArgs& a, long long step, c
     return si;
 }
 
+// Row stream of a workgroup.  Per-plane mode: one segment = rows 0..H-1 of one plane.
+// Split mode (row_split > 0): the P*H rows of all planes, concatenated, are cut into equal
+// contiguous ranges of CORE rows, one per workgroup, so that every CU gets work even when
+// P < #CUs.  A range may span several planes (segments, at most SP_MAXSEG); where it starts or
+// ends inside a plane it is extended by n_tv halo rows, which are computed (with the plane
+// edge treated as a boundary) but neither stored nor counted: the TV dependency cone grows by
+// one row per inner iteration, so after n_tv iterations the core rows are exact.  Interior
+// segment boundaries are true plane edges.  All fields are workgroup-uniform (SGPRs).
+struct RowMap {
+    int ns;                      // segments (1 .. SP_MAXSEG)
+    int Q;                       // stream rows (halo included)
+    int htop, hbot;              // halo rows at the start / end of the stream
+    int q1, q2, q3;              // stream index of segments 1..3 (Q when absent); segment 0 starts at 0
+    int pl0, pl1, pl2, pl3;      // plane of each segment
+    int lo0, lo1, lo2, lo3;      // plane row of each segment's first stream row
+    // (scalar members, not arrays: the struct must stay in SGPRs)
+    __device__ __forceinline__ int qs(int s) const { return s <= 0 ? 0 : (s == 1 ? q1 : (s == 2 ? q2 : (s == 3 ? q3 : Q))); }
+    __device__ __forceinline__ int pl(int s) const { return s == 0 ? pl0 : (s == 1 ? pl1 : (s == 2 ? pl2 : pl3)); }
+    __device__ __forceinline__ int lo(int s) const { return s == 0 ? lo0 : (s == 1 ? lo1 : (s == 2 ? lo2 : lo3)); }
+};
+
+__device__ __forceinline__ void build_rowmap(const TvArgs& a, int wg, RowMap& m) {
+    const int H = a.H;
+    m.pl0 = m.pl1 = m.pl2 = m.pl3 = 0;
+    m.lo0 = m.lo1 = m.lo2 = m.lo3 = 0;
+    if (a.split_wgs <= 0) {
+        m.ns = 1; m.Q = H; m.htop = 0; m.hbot = 0;
+        m.q1 = m.q2 = m.q3 = H;
+        m.pl0 = wg / a.nsegs;
+        return;
+    }
+    const long long T = (long long)a.B * a.C * H;
+    const long long g0 = T * wg / a.split_wgs, g1 = T * (wg + 1) / a.split_wgs;
+    const int p0 = (int)(g0 / H), p1 = (int)((g1 - 1) / H);
+    const int h = a.n_tv;
+    m.ns = p1 - p0 + 1;
+    // segment s covers plane p0 + s; only the first can start and the last can end inside it
+    auto seg = [&](int s, int& lo, int& len, int& ht, int& hb) {
+        const int p = p0 + s;
+        const int clo = (s == 0) ? (int)(g0 - (long long)p * H) : 0;
+        const int chi = (p == p1) ? (int)(g1 - (long long)p * H) : H;
+        lo = clo > 0 ? max(0, clo - h) : 0;
+        const int hi = chi < H ? min(H, chi + h) : H;
+        len = hi - lo;
+        ht = clo - lo;
+        hb = hi - chi;
+    };
+    int lo, len, ht, hb;
+    seg(0, lo, len, ht, hb);
+    m.pl0 = p0; m.lo0 = lo; m.htop = ht; m.hbot = hb;
+    int q = len;
+    m.q1 = m.q2 = m.q3 = 0;
+    if (m.ns > 1) { seg(1, lo, len, ht, hb); m.q1 = q; m.pl1 = p0 + 1; m.lo1 = lo; m.hbot = hb; q += len; }
+    if (m.ns > 2) { seg(2, lo, len, ht, hb); m.q2 = q; m.pl2 = p0 + 2; m.lo2 = lo; m.hbot = hb; q += len; }
+    if (m.ns > 3) { seg(3, lo, len, ht, hb); m.q3 = q; m.pl3 = p0 + 3; m.lo3 = lo; m.hbot = hb; q += len; }
+    m.Q = q;
+    if (m.ns <= 1) m.q1 = q;
+    if (m.ns <= 2) m.q2 = q;
+    if (m.ns <= 3) m.q3 = q;
+}
+
+// Position of a role's current row in the stream; advanced monotonically (the segment walk
+// runs only when a plane boundary is crossed).
+struct RowCursor {
+    int q, s, p, r, qend;
+};
+__device__ __forceinline__ void cursor_seek(const RowMap& m, RowCursor& c) {
+    while (c.s + 1 < m.ns && c.q >= m.qs(c.s + 1)) ++c.s;
+    c.qend = m.qs(c.s + 1);
+    c.p = m.pl(c.s);
+    c.r = m.lo(c.s) + (c.q - m.qs(c.s));
+}
+__device__ __forceinline__ void cursor_init(const RowMap& m, RowCursor& c, int q) {
+    c.q = q; c.s = 0;
+    cursor_seek(m, c);
+}
+__device__ __forceinline__ void cursor_advance(const RowMap& m, RowCursor& c, int d) {
+    c.q += d; c.r += d;
+    if (c.q >= c.qend && c.s + 1 < m.ns) cursor_seek(m, c);
+}
+// stream index of the first segment start after stream row q (SP_NOSEG if none)
+__device__ __forceinline__ int next_seg_start(const RowMap& m, int q) {
+    if (m.ns > 1 && m.q1 > q) return m.q1;
+    if (m.ns > 2 && m.q2 > q) return m.q2;
+    if (m.ns > 3 && m.q3 > q) return m.q3;
+    return SP_NOSEG;
+}
+
 // One pipeline stage = one inner TV iteration on one row pair.  Phase A (primal) on the
 // lookahead row j from ring k-1; phase B (dual) on the output row i = j-1, which needs z of
 // rows i (held from the previous step) and j.
@@ -726,21 +817,42 @@ __device__ __forceinline__ void stage_phase_b(const TvArgs& a, const StageRow& r
     }
 }
 
-// Stage k's whole life over the plane.  At step t the stage (lookahead row j = t - 3k - 1)
+// Stage k's whole life over the row stream.  At step t the stage (lookahead row j = t - 3k - 1)
 //   1. issues the LDS reads of ring k-1 row j,
 //   2. runs the dual update of row i = j - 2 -- every input is already in registers (z of
 //      rows i and i+1 from the two previous steps) -- and writes row i to ring k,
 //   3. runs the primal update of row j once the reads have landed.
 // The ring reads' latency and the ring writes thus overlap computation instead of
 // bracketing it.  Three row states rotate (RA -> RB -> RC) so nothing is copied.
+// Segment edges (split mode): the first row of a segment has no row above (its primal
+// uses u0 = 0 above) and the last has no row below (its dual has no vertical difference);
+// the rel-err partial sums are flushed per segment (different segments may be different chains).
 template <bool EXACT, bool TRK>
-__device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, int k, int nsteps, int lane,
-                                           bool last3, bool core, float& sd, float& sn, Stamps& stp) {
-    const int H = a.H;
+__device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, const RowMap& rm, int k, int nsteps,
+                                           int lane, bool last3, bool core, Stamps& stp) {
+    const int Q = rm.Q;
     const int tbeg = 1 + 3 * k;          // step of lookahead row 0
     StageRow RA, RB, RC;
     const float zero[CPL] = {0.f, 0.f, 0.f, 0.f};
-    float lsd = 0.f, lsn = 0.f;
+    float lsd = 0.f, lsn = 0.f;          // rel-err partial sums of segment sacc (core rows)
+    int sacc = 0;
+    int nb = next_seg_start(rm, 0);      // next segment start after the current primal row
+    bool fprev = false;                  // row j-1 started a segment
+    const int qc0 = rm.htop, qc1 = Q - rm.hbot;   // core stream rows
+    auto flush = [&]() {
+        if (TRK) {
+            const float d = wave_sum(core ? lsd : 0.f);
+            const float q = wave_sum(core ? lsn : 0.f);
+            if (lane == 0) { sh.red[sacc][k - 1][0] = d; sh.red[sacc][k - 1][1] = q; }
+            lsd = 0.f; lsn = 0.f;
+        }
+    };
+    auto primal = [&](int j, const float4& X2, const float4& U0, const float4& U1, const float4& YY,
+                      const float (&pu0)[CPL], StageRow& cur) {
+        float rd = 0.f, rn = 0.f;
+        stage_phase_a<EXACT, TRK>(a, X2, U0, U1, YY, pu0, cur, rd, rn);
+        if (TRK && j >= qc0 && j < qc1) { lsd += rd; lsn += rn; }
+    };
     int t = 0;
     for (; t < tbeg; ++t) step_barrier(stp);
     auto load_row = [&](int j, float4& X2, float4& U0, float4& U1, float4& YY) {
@@ -756,46 +868,56 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, in
         sh.u0[k][so][lane] = make_float4(un0[0], un0[1], un0[2], un0[3]);
         sh.u1[k][so][lane] = make_float4(un1[0], un1[1], un1[2], un1[3]);
     };
-    // rows 0 and 1: primal update only
+    // rows 0 and 1: primal update only (segments hold >= 2 rows: row 1 never starts one)
     {
         float4 X2, U0, U1, YY;
         load_row(0, X2, U0, U1, YY);
-        stage_phase_a<EXACT, TRK>(a, X2, U0, U1, YY, zero, RA, lsd, lsn);
+        primal(0, X2, U0, U1, YY, zero, RA);
         step_barrier(stp);
         load_row(1, X2, U0, U1, YY);
-        stage_phase_a<EXACT, TRK>(a, X2, U0, U1, YY, RA.u0, RB, lsd, lsn);
+        primal(1, X2, U0, U1, YY, RA.u0, RB);
         step_barrier(stp);
         t += 2;
     }
-    // middle rows j = 2..H-1: dual update of row j-2 (p2) with z of row j-1 (p1), then primal of j
+    // middle rows j = 2..Q-1: dual update of row j-2 (p2) with z of row j-1 (p1), then primal of j
     auto middle = [&](int j, StageRow& p2, StageRow& p1, StageRow& cur) {
         float4 X2, U0, U1, YY;
         load_row(j, X2, U0, U1, YY);
         float un0[CPL], un1[CPL];
-        stage_phase_b<EXACT, true>(a, p2, p1.z, last3, un0, un1);
+        if (!fprev) stage_phase_b<EXACT, true>(a, p2, p1.z, last3, un0, un1);
+        else stage_phase_b<EXACT, false>(a, p2, zero, last3, un0, un1);   // row j-2 ends a segment
         store_row(j - 2, p2, un0, un1);
-        stage_phase_a<EXACT, TRK>(a, X2, U0, U1, YY, p1.u0, cur, lsd, lsn);
+        const bool fj = j == nb;
+        if (fj) {                       // row j starts a new segment (split mode only)
+            flush();
+            ++sacc;
+            nb = next_seg_start(rm, j);
+            primal(j, X2, U0, U1, YY, zero, cur);
+        } else {
+            primal(j, X2, U0, U1, YY, p1.u0, cur);
+        }
+        fprev = fj;
         step_barrier(stp);
     };
     int j = 2;
-    for (; j + 2 < H; j += 3) {
+    for (; j + 2 < Q; j += 3) {
         middle(j, RA, RB, RC);
         middle(j + 1, RB, RC, RA);
         middle(j + 2, RC, RA, RB);
     }
     t += (j - 2);
-    // j = H: dual update of row H-2 (z of row H-1 known); j = H+1: row H-1 (no row below).
+    // j = Q: dual update of row Q-2 (z of row Q-1 known); j = Q+1: row Q-1 (no row below).
     // (static buffer roles per remainder: a runtime-indexed StageRow would go to scratch)
     auto finish = [&](StageRow& r2, StageRow& r1) {
         float un0[CPL], un1[CPL];
         stage_phase_b<EXACT, true>(a, r2, r1.z, last3, un0, un1);
-        store_row(H - 2, r2, un0, un1);
+        store_row(Q - 2, r2, un0, un1);
         step_barrier(stp);
         stage_phase_b<EXACT, false>(a, r1, zero, last3, un0, un1);
-        store_row(H - 1, r1, un0, un1);
+        store_row(Q - 1, r1, un0, un1);
         step_barrier(stp);
     };
-    const int rem = H - j;              // 0, 1 or 2 middle rows left
+    const int rem = Q - j;              // 0, 1 or 2 middle rows left
     if (rem == 0) {
         finish(RA, RB);
     } else if (rem == 1) {
@@ -808,7 +930,7 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, in
     }
     t += rem + 2;
     for (; t < nsteps; ++t) step_barrier(stp);
-    if (core) { sd += lsd; sn += lsn; }
+    flush();
 }
 
 template <bool EXACT, bool ALPHA1>
@@ -820,10 +942,12 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     const int H = a.H, W = a.W, C = a.C;
     const long long step = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
     const bool fresh = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
-    const int plane = blockIdx.x / a.nsegs;
-    const int seg = blockIdx.x - plane * a.nsegs;
-    const int b = plane / C, c = plane - b * C;
-    const int cc0 = seg * a.seg_w, cc1 = min(W, cc0 + a.seg_w);
+    RowMap rm;
+    build_rowmap(a, blockIdx.x, rm);
+    const int Q = rm.Q;
+    const int qc0 = rm.htop, qc1 = Q - rm.hbot;          // core stream rows
+    const int cseg = a.split_wgs > 0 ? 0 : blockIdx.x - (blockIdx.x / a.nsegs) * a.nsegs;
+    const int cc0 = cseg * a.seg_w, cc1 = min(W, cc0 + a.seg_w);
     const int f0 = max(0, cc0 - a.halo) & ~3;
     const int gj0 = f0 + CPL * lane;
     const bool lane_ok = gj0 < W;
@@ -831,9 +955,8 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     const size_t HW = (size_t)H * W;
     const size_t E = (size_t)C * HW;
     const size_t BE = (size_t)a.B * E;
-    const size_t plane_off = (size_t)b * E + (size_t)c * HW;
     const int par_in = (int)(step & 1), par_out = (int)((step + 1) & 1);
-    const int nsteps = H + 4 + 3 * n;
+    const int nsteps = Q + 4 + 3 * n;
     const int role = (w < SP_FRONT) ? 0 : (w < SP_FRONT + n ? 1 : 2);
     const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
     Stamps stp;
@@ -842,15 +965,15 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     stp.w = w;
     stp.tr = (a.stamps && blockIdx.x == 0) ? a.stamps + (size_t)gridDim.x * 32 : nullptr;
 #endif
+    auto plane_off = [&](int pl) -> size_t { return (size_t)pl * HW; };   // planes are (b, c) in NCHW order
 
-    float sd = 0.f, sn = 0.f;
     const int k_st = w - SP_FRONT + 1;                 // inner TV iteration (1-based)
     const bool trk = role == 1 && (k_st - 1) >= 2 && (k_st - 1) <= n - 2;
     // Each role runs its own loop (its state is live only there); every wave executes
     // exactly nsteps barriers, so the s_barrier instances pair up across roles.
     if (role == 0) {
         // ---------------- FRONT state ----------------
-        const int fw = w;                                  // front wave id (rows r % 4 == fw)
+        const int fw = w;                                  // front wave id (stream rows q % 4 == fw)
         uint32_t ph0 = 0, ph1 = 0, ph2 = 0, ph3 = 0;
         float zn0 = 0.f, zn1 = 0.f, zn2 = 0.f, zn3 = 0.f;
         const float* xin = a.x[par_in];
@@ -859,28 +982,34 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
         // The loads of a row are LDS-DMA'd 4 steps before the row is consumed (double-buffered
         // per front wave), row and column clamped into the plane so every lane loads.
         const int gjc = min(gj0, W - CPL);
-        auto front_issue = [&](int r) {
-            const int rc = min(r, H - 1);
-            const int bi = (r >> 2) & 1;
-            const size_t base = plane_off + (size_t)rc * W + gjc;
+        RowCursor rc_cur, rc_dma;
+        cursor_init(rm, rc_cur, min(fw, Q - 1));
+        cursor_init(rm, rc_dma, min(fw, Q - 1));
+        auto front_issue = [&](int q, const RowCursor& rc) {
+            const int rr = min(rc.r, H - 1);
+            const int bi = (q >> 2) & 1;
+            const int bb = rc.p / C;
+            const size_t base = plane_off(rc.p) + (size_t)rr * W + gjc;
             glds16(xin + base, &sh.fst[fw][bi][0][0]);
-            glds16(a.yobs + (size_t)b * a.y_cs + (size_t)c * HW + (size_t)rc * W + gjc, &sh.fst[fw][bi][1][0]);
+            glds16(a.yobs + (size_t)bb * a.y_cs + (size_t)(rc.p - bb * C) * HW + (size_t)rr * W + gjc,
+                   &sh.fst[fw][bi][1][0]);
             glds16(u2in + 2 * base, &sh.fst[fw][bi][2][0]);
             glds16(u2in + 2 * base + 4, &sh.fst[fw][bi][3][0]);
             if (!ALPHA1) glds16(x2in + base, &sh.fst[fw][bi][4][0]);
-            glds4(a.mask + (size_t)b * a.m_cs + (size_t)rc * W + gjc, &sh.fmk[fw][bi][0]);
+            glds4(a.mask + (size_t)bb * a.m_cs + (size_t)rr * W + gjc, &sh.fmk[fw][bi][0]);
         };
-        front_issue(fw);
+        front_issue(fw, rc_dma);
         for (int t = 0; t < nsteps; ++t) {
                 // ======================= FRONT =======================
                 const int p = (t + 4 - fw) & 3;
-                const int r = t - p;
-                if (r >= 0 && r < H) {
+                const int q = t - p;
+                if (q >= 0 && q < Q) {
                     if (p == 0) {
-                        const size_t e = ((size_t)c * H + r) * W + gj0;
+                        const int bb = rc_cur.p / C, cc = rc_cur.p - bb * C;
+                        const size_t e = ((size_t)cc * H + rc_cur.r) * W + gj0;
                         uint32_t c0 = (uint32_t)(e >> 2), c1 = (uint32_t)step, c2 = TAG_LANGEVIN,
                                  c3 = (uint32_t)(a.seed >> 32);
-                        philox4x32_10(c0, c1, c2, c3, (uint32_t)a.seed, (uint32_t)(a.chain0 + b));
+                        philox4x32_10(c0, c1, c2, c3, (uint32_t)a.seed, (uint32_t)(a.chain0 + bb));
                         ph0 = c0; ph1 = c1; ph2 = c2; ph3 = c3;
                     } else if (p == 1) {
                         box_muller(ph0, ph1, zn0, zn1);
@@ -888,9 +1017,9 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
                         box_muller(ph2, ph3, zn2, zn3);
                     } else {
                         STAMP_START(stp);
-                        wait_vm0();   // this wave's DMA of row r (issued 4 steps ago)
+                        wait_vm0();   // this wave's DMA of row q (issued 4 steps ago)
                         STAMP_SEG(stp, 0);
-                        const int bi = (r >> 2) & 1;
+                        const int bi = (q >> 2) & 1;
                         const float4 fX = sh.fst[fw][bi][0][lane];
                         const float4 fYo = sh.fst[fw][bi][1][lane];
                         const float4 fU0 = sh.fst[fw][bi][2][lane];
@@ -913,14 +1042,17 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
                         if (fresh) x2s = Y4;
                         else x2s = ALPHA1 ? fX : fXS;
                         if (!lane_ok) x2s = zero4;
-                        const int s0 = r & 1;
+                        const int s0 = q & 1;
                         STAMP_SEG(stp, 1);
                         sh.x2[0][s0][lane] = x2s;
                         sh.u0[0][s0][lane] = fresh ? zero4 : make_float4(fU0.x, fU0.z, fU1.x, fU1.z);
                         sh.u1[0][s0][lane] = fresh ? zero4 : make_float4(fU0.y, fU0.w, fU1.y, fU1.w);
-                        sh.y[r & (SP_YRING - 1)][lane] = Y4;
+                        sh.y[q & (SP_YRING - 1)][lane] = Y4;
                         STAMP_SEG(stp, 2);
-                        front_issue(r + 4);   // into the buffer of row r - 4 (consumed 4 steps ago)
+                        // the wave's next rows: noise row q + 4, DMA of row q + 8... issued as q + 4
+                        cursor_advance(rm, rc_cur, 4);
+                        if (q + 4 < Q) cursor_advance(rm, rc_dma, 4);
+                        front_issue(q + 4, rc_dma);   // into the buffer of row q - 4 (consumed 4 steps ago)
                         STAMP_SEG(stp, 3);
                     }
                 }
@@ -932,39 +1064,43 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
         // the left edge, the last row of u2[...,0] and the last column of u2[...,1] need no
         // select: the DPP shift feeds 0 at lane 0 and TV keeps those dual components exactly 0.
         const bool last3 = gj0 + CPL - 1 == W - 1;
-        if (trk) stage_loop<EXACT, true>(a, sh, k_st, nsteps, lane, last3, core, sd, sn, stp);
-        else stage_loop<EXACT, false>(a, sh, k_st, nsteps, lane, last3, core, sd, sn, stp);
+        if (trk) stage_loop<EXACT, true>(a, sh, rm, k_st, nsteps, lane, last3, core, stp);
+        else stage_loop<EXACT, false>(a, sh, rm, k_st, nsteps, lane, last3, core, stp);
     } else {
         // ---------------- BACK state ----------------
-        const int bw = w - SP_FRONT - n;                   // back wave id (rows r % 2 == bw)
+        const int bw = w - SP_FRONT - n;                   // back wave id (stream rows q % 2 == bw)
         const StepInfo si = step_info(a, step, a.mean[par_out]);
         const float* mean_in = a.mean[par_in];
         const float* sq_in = a.sq[par_in];
         const bool need_prev = si.acc && !si.first;
         const int gjc = min(gj0, W - CPL);
-        auto back_issue = [&](int r) {
+        RowCursor rc_cur, rc_dma;
+        cursor_init(rm, rc_cur, min(bw, Q - 1));
+        cursor_init(rm, rc_dma, min(bw, Q - 1));
+        auto back_issue = [&](int q, const RowCursor& rc) {
             if (need_prev) {
-                const int rc = min(r, H - 1);
-                const int bi = (r >> 1) & 1;
-                const size_t base = plane_off + (size_t)rc * W + gjc;
+                const int rr = min(rc.r, H - 1);
+                const int bi = (q >> 1) & 1;
+                const size_t base = plane_off(rc.p) + (size_t)rr * W + gjc;
                 glds16(mean_in + base, &sh.bst[bw][bi][0][0]);
                 glds16(sq_in + base, &sh.bst[bw][bi][1][0]);
             }
         };
-        // vector-memory stores per row (all lanes of a wave store together; lane 0 is core)
+        // vector-memory stores per core row (all lanes of a wave store together; lane 0 is core)
         const int nst = 3 + (ALPHA1 ? 0 : 1) + ((si.acc && (si.blockend || si.liveout)) ? 2 : 0) + (si.sample ? 1 : 0);
-        back_issue(bw);
+        int pend = 0;   // stores issued after the DMA of the current row
+        back_issue(bw, rc_dma);
         for (int t = 0; t < nsteps; ++t) {
                 // ======================= BACK =======================
-                const int r = t - 4 - 3 * n;
-                if (r >= 0 && r < H && (r & 1) == bw) {
-                    const int sl = r & 1;
+                const int q = t - 4 - 3 * n;
+                if (q >= 0 && q < Q && (q & 1) == bw) {
+                    const int sl = q & 1;
                     const float4 X2 = sh.x2[n][sl][lane];
                     const float4 U0 = sh.u0[n][sl][lane];
                     const float4 U1 = sh.u1[n][sl][lane];
                     float4 Xo = X2;
                     if (!ALPHA1) {
-                        const float4 YY = sh.y[r & (SP_YRING - 1)][lane];
+                        const float4 YY = sh.y[q & (SP_YRING - 1)][lane];
                         Xo.x = (1.0f - a.alpha) * YY.x + a.alpha * X2.x;
                         Xo.y = (1.0f - a.alpha) * YY.y + a.alpha * X2.y;
                         Xo.z = (1.0f - a.alpha) * YY.z + a.alpha * X2.z;
@@ -974,35 +1110,40 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
                     if (si.acc) {
                         float4 bm = zero4, bq = zero4;
                         if (need_prev) {
-                            // DMA of row r was issued just before the previous row's nst stores
-                            wait_vm_n(r == bw ? 0 : nst);
-                            bm = sh.bst[bw][(r >> 1) & 1][0][lane];
-                            bq = sh.bst[bw][(r >> 1) & 1][1][lane];
+                            // DMA of row q was issued just before the previous row's stores
+                            wait_vm_n(pend);
+                            bm = sh.bst[bw][(q >> 1) & 1][0][lane];
+                            bq = sh.bst[bw][(q >> 1) & 1][1][lane];
                         }
                         const float xs[CPL] = {Xo.x, Xo.y, Xo.z, Xo.w};
                         const float ms[CPL] = {bm.x, bm.y, bm.z, bm.w};
                         const float qs[CPL] = {bq.x, bq.y, bq.z, bq.w};
-                        float m[CPL], q[CPL];
+                        float m[CPL], qq[CPL];
 #pragma unroll
                         for (int kk = 0; kk < CPL; ++kk) {
                             if (si.first) {
                                 m[kk] = si.cb * xs[kk];
-                                q[kk] = si.cb * (xs[kk] * xs[kk]);
+                                qq[kk] = si.cb * (xs[kk] * xs[kk]);
                             } else {
                                 m[kk] = si.ca * ms[kk] + si.cb * xs[kk];
-                                q[kk] = si.ca * qs[kk] + si.cb * (xs[kk] * xs[kk]);
+                                qq[kk] = si.ca * qs[kk] + si.cb * (xs[kk] * xs[kk]);
                             }
                         }
                         M4 = make_float4(m[0], m[1], m[2], m[3]);
-                        Q4 = make_float4(q[0], q[1], q[2], q[3]);
+                        Q4 = make_float4(qq[0], qq[1], qq[2], qq[3]);
                     }
                     // all LDS reads of this row (ring + staging) done before the staging
                     // buffer is re-targeted by the next DMA
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    back_issue(r + 2);
+                    const RowCursor rc = rc_cur;
+                    cursor_advance(rm, rc_cur, 2);
+                    if (q + 2 < Q) cursor_advance(rm, rc_dma, 2);
+                    back_issue(q + 2, rc_dma);
                     asm volatile("" ::: "memory");
-                    if (core) {
-                        const size_t base = plane_off + (size_t)r * W + gj0;
+                    const bool rowcore = q >= qc0 && q < qc1;
+                    pend = rowcore ? nst : 0;
+                    if (rowcore && core) {
+                        const size_t base = plane_off(rc.p) + (size_t)rc.r * W + gj0;
                         *reinterpret_cast<float4*>(a.x[par_out] + base) = Xo;
                         float* u2o = a.u2[par_out] + 2 * base;
                         *reinterpret_cast<float4*>(u2o) = make_float4(U0.x, U1.x, U0.y, U1.y);
@@ -1034,18 +1175,17 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
         }
     }
 #endif
-    // rel_err partial sums of this plane -> global (deepinv's early-stop test, per chain)
-    if (role == 1 && trk) {
-        sd = wave_sum(sd);
-        sn = wave_sum(sn);
-        if (lane == 0) { sh.red[k_st - 1][0] = sd; sh.red[k_st - 1][1] = sn; }
-    }
+    // rel_err partial sums of this stream -> global, per segment's chain (deepinv's
+    // early-stop test, per chain); the tracking stages wrote sh.red[segment][k - 1]
     lds_barrier();
-    if (threadIdx.x >= 2 && (int)threadIdx.x <= n - 2) {
-        const int tt = threadIdx.x;
-        const int g = a.per_chain_norm ? b : 0;
-        atomicAdd(&a.norms[((size_t)g * a.n_tv + tt) * 2], (double)sh.red[tt][0]);
-        atomicAdd(&a.norms[((size_t)g * a.n_tv + tt) * 2 + 1], (double)sh.red[tt][1]);
+    for (int tt = threadIdx.x; tt < SP_MAXSEG * SP_MAXST; tt += blockDim.x) {
+        const int sg = tt / SP_MAXST, it = tt - sg * SP_MAXST;     // it = k - 1
+        if (sg < rm.ns && it >= 2 && it <= n - 2) {
+            const int pl = rm.pl(sg);
+            const int g = a.per_chain_norm ? pl / C : 0;
+            atomicAdd(&a.norms[((size_t)g * a.n_tv + it) * 2], (double)sh.red[sg][it][0]);
+            atomicAdd(&a.norms[((size_t)g * a.n_tv + it) * 2 + 1], (double)sh.red[sg][it][1]);
+        }
     }
 }
 
@@ -1260,6 +1400,38 @@ static void tv_tiling(TvArgs& a) {
     a.tiles = a.nbands * a.nsegs;
 }
 
+static int device_cus() {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return 256;
+    return cus;
+}
+
+// Row-split workgroup count for the streaming kernel (0 = one workgroup per plane).
+// req: 0 auto, -1 per plane, > 0 forced.  A range of R rows touches at most ceil(R/H) + 1
+// planes, so R <= 3H keeps it within SP_MAXSEG = 4 segments: G >= ceil(P/3).
+static int choose_split(int B, int C, int H, int W, int h, int req, int* out) {
+    const long long P = (long long)B * C, T = P * H;
+    const long long gmin = (P + SP_MAXSEG - 2) / (SP_MAXSEG - 1);
+    *out = 0;
+    if (req < 0) return 0;
+    if (req > 0) {
+        if (W > TV_COLS) return fail(0, "psgla_tv_step: stream_wgs > 0 needs W <= 256");
+        if (req < gmin || req > T) return fail(0, "psgla_tv_step: stream_wgs outside [ceil(B*C/3), B*C*H]");
+        *out = req;
+        return 0;
+    }
+    if (W > TV_COLS) return 0;
+    const long long cus = device_cus();
+    if (P > (SP_MAXSEG - 1) * cus) return 0;          // enough planes: one workgroup each
+    long long g = (T + 4LL * h - 1) / (4LL * h);      // >= 4 n_tv core rows per range
+    if (g > cus) g = cus;
+    if (g < gmin) g = gmin;
+    if (g <= P && T % g == 0 && (T / g) % H == 0) return 0;   // ranges = whole planes anyway
+    *out = (int)g;
+    return 0;
+}
+
 template <bool EXACT, int FRONT, bool ALPHA1>
 static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
     const int P = a.B * a.C;
@@ -1277,7 +1449,8 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
                 s.seg_w = (((a.W + s.nsegs - 1) / s.nsegs) + 3) & ~3;
             }
             const int threads = WAVE * (SP_FRONT + a.n_tv + SP_BACK);
-            hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1>), dim3(P * s.nsegs), dim3(threads), 0, st, s);
+            const int grid = s.split_wgs > 0 ? s.split_wgs : P * s.nsegs;
+            hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1>), dim3(grid), dim3(threads), 0, st, s);
         } else {
             const int grid_main = ((P + 7) / 8) * 8 * a.tiles;
             hipLaunchKernelGGL((tv_main_kernel<EXACT, FRONT, ALPHA1>), dim3(grid_main), dim3(TV_THREADS), 0, st, a);
@@ -1339,6 +1512,11 @@ int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream) {
     const bool streamable = (d->W % 4 == 0) && d->n_tv >= 1 && d->n_tv <= SP_MAXST && d->H >= 2;
     a.stream = streamable && d->kernel_variant != 1;
     if (d->kernel_variant == 2 && !streamable) return fail(0, "psgla_tv_step: shape not supported by the streaming kernel");
+    a.split_wgs = 0;
+    if (a.stream) {
+        const int rc = choose_split(d->B, d->C, d->H, d->W, d->n_tv, d->stream_wgs, &a.split_wgs);
+        if (rc) return rc;
+    }
     hipStream_t st = (hipStream_t)stream;
     const int m = d->launch_mask;
     if (d->exact)

@@ -24,7 +24,8 @@ class FusedTvChains:
                  sigma2: float, alpha: float, ths: float, tv: K.TvConstants, seed: int, n_iter: int,
                  n_inter: int, n_inter_mmse: int, chain0: int = 0, exact: bool = False,
                  tv_x2: torch.Tensor | None = None, tv_u2: torch.Tensor | None = None,
-                 store_samples: bool = True, store_blocks: bool = True, kernel_variant: str = "auto"):
+                 store_samples: bool = True, store_blocks: bool = True, kernel_variant: str = "auto",
+                 stream_wgs: int = 0):
         if init.dim() != 4:
             raise ValueError("init must be (B, C, H, W)")
         if tv.n_it > N.TV_MAX_FUSED_IT:
@@ -81,6 +82,7 @@ class FusedTvChains:
         d.norms = self.work.norms.data_ptr()
         d.arrive = self.work.arrive.data_ptr()
         d.kernel_variant = {"auto": 0, "band": 1, "stream": 2}[kernel_variant]
+        d.stream_wgs = int(stream_wgs)
         self.desc = d
         self.sched_struct = self.sched.struct(True, 0)
         if self.warm_first:

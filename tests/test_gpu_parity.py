@@ -153,7 +153,7 @@ def test_fused_psgla_tv_fast_within_tolerance():
     assert Xl.shape == fx["samples"].shape
 
 
-def _fused_batch(B, chain0, exact, n_iter=40, H=48, W=64, alpha=1.0, variant="auto"):
+def _fused_batch(B, chain0, exact, n_iter=40, H=48, W=64, alpha=1.0, variant="auto", stream_wgs=0):
     from psgla_for_posterior_sampling_amd.engine import FusedTvChains
     from psgla_for_posterior_sampling_amd import hip_ops as K
     g = torch.Generator().manual_seed(5)
@@ -164,7 +164,7 @@ def _fused_batch(B, chain0, exact, n_iter=40, H=48, W=64, alpha=1.0, variant="au
                         mask2d.to(torch.uint8).to(DEV), c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
                         alpha=alpha, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10), seed=3,
                         n_iter=n_iter, n_inter=5, n_inter_mmse=4, chain0=chain0, exact=exact,
-                        kernel_variant=variant)
+                        kernel_variant=variant, stream_wgs=stream_wgs)
     return eng, (dg, y, init, mask2d, c1, c2)
 
 
@@ -200,6 +200,49 @@ def test_fused_multichain_exact_vs_oracle(variant, H, W):
         bm, bm2 = eng.blocks()
         np.testing.assert_array_equal(bm[:, b].cpu().numpy(), np.stack([t.numpy() for t in Ml]))
         np.testing.assert_array_equal(bm2[:, b].cpu().numpy(), np.stack([t.numpy() for t in M2l]))
+
+
+_ORACLE_CACHE = {}
+
+
+def _oracle_chain(init, dg, n_iter, chain):
+    key = (n_iter, chain, tuple(init.shape))
+    if key not in _ORACLE_CACHE:
+        tv = orc.TVDenoiser(n_it_max=10)
+        Xl, Ml, M2l = orc.psgla(init, dg, tv, torch.tensor(1.0), torch.tensor(10.0), sig_float=10 / 255.0,
+                                delta=(10 / 255.0) ** 2, n_iter=n_iter, n_inter=5, n_inter_mmse=4, seed=3,
+                                chain=chain)
+        _ORACLE_CACHE[key] = (np.stack([t.numpy() for t in Xl]), np.stack([t.numpy() for t in Ml]),
+                              np.stack([t.numpy() for t in M2l]), tv.x2.numpy(), tv.u2.numpy())
+    return _ORACLE_CACHE[key]
+
+
+@pytest.mark.parametrize("stream_wgs", [-1, 3, 4, 7, 11, 20, 97])
+def test_stream_row_split_exact_vs_oracle(stream_wgs):
+    """Row-split streaming (the plane rows of all chains cut into stream_wgs ranges, n_tv halo rows
+    at cuts inside a plane, ranges spanning plane boundaries): bit-identical to the checker for
+    every cut position; -1 = one workgroup per plane."""
+    B, H, W, n_iter = 3, 48, 64, 20
+    eng, (dg, y, init, mask2d, c1, c2) = _fused_batch(B, 10, exact=True, n_iter=n_iter, H=H, W=W,
+                                                      variant="stream", stream_wgs=stream_wgs)
+    eng.run(n_iter, graph_steps=0)
+    torch.cuda.synchronize()
+    bm, bm2 = eng.blocks()
+    for b in range(B):
+        Xs, Ms, M2s, x2, u2 = _oracle_chain(init, dg, n_iter, 10 + b)
+        np.testing.assert_array_equal(eng.samples()[:, b].cpu().numpy(), Xs)
+        np.testing.assert_array_equal(bm[:, b].cpu().numpy(), Ms)
+        np.testing.assert_array_equal(bm2[:, b].cpu().numpy(), M2s)
+        np.testing.assert_array_equal(eng.u2_state[b].cpu().numpy(), u2[0])
+
+
+def test_stream_row_split_rejects_bad_counts():
+    from psgla_for_posterior_sampling_amd._native import NativeLibraryError
+    for bad in (1, 10 ** 6):           # fewer than ceil(B*C/3) ranges / more ranges than rows
+        with pytest.raises((RuntimeError, NativeLibraryError)):
+            eng, _ = _fused_batch(3, 0, exact=True, n_iter=10, variant="stream", stream_wgs=bad)
+            eng.run(1, graph_steps=0)
+            torch.cuda.synchronize()
 
 
 @pytest.mark.parametrize("variant", ["stream", "band"])

@@ -18,6 +18,8 @@ p.add_argument("--steps", type=int, default=30)
 p.add_argument("--batch", type=int, default=64)
 p.add_argument("--exact", action="store_true")
 p.add_argument("--main-only", type=int, default=0, help="extra tile-kernel-only launches")
+p.add_argument("--stream-wgs", type=int, default=0)
+p.add_argument("--tv-iters", type=int, default=10)
 a = p.parse_args()
 dev = torch.device("cuda:0")
 B, C, H, W = a.batch, 3, 256, 256
@@ -33,8 +35,8 @@ c1 = float((torch.tensor(s * s).float() / torch.tensor(10.0)).item())
 c2 = float((torch.tensor(np.sqrt(2)).float() * torch.tensor(s).float()).item())
 eng = FusedTvChains(init.contiguous(), y.contiguous(), mask_2d.to(torch.uint8), c1=c1, c2=c2,
                     sigma2=float(np.float32((1 / 255.0) ** 2)), alpha=1.0, ths=float(np.float32(s)),
-                    tv=K.TvConstants(n_it_max=10), seed=0, n_iter=a.steps, n_inter=10, n_inter_mmse=10,
-                    exact=a.exact)
+                    tv=K.TvConstants(n_it_max=a.tv_iters), seed=0, n_iter=a.steps, n_inter=10, n_inter_mmse=10,
+                    exact=a.exact, stream_wgs=a.stream_wgs)
 eng.step(a.steps)
 if a.main_only:
     eng.launch_main_only(a.main_only)
