@@ -61,6 +61,7 @@ struct TvArgs {
     const uint8_t* mask;
     long long m_cs;
     float c1, c2, sigma2, alpha;
+    float inv_sigma2;               // fast kernels: 1/sigma2 (the data term multiplies)
     float tau, opt, inv_opt, sig_tv, rho, ths, tol;
     int n_tv;
     unsigned long long seed;
@@ -86,6 +87,8 @@ struct TvArgs {
     int nbands, band_h, nsegs, seg_w, tiles, halo;
     int stream;                     // 1: main pass = row-streaming pipeline kernel
     int split_wgs;                  // stream kernel: > 0 = row-split mode over this many workgroups
+    int st_nsegs, st_seg_w, st_halo;  // stream kernel column segmentation (W > 256)
+    int fin_inline;                 // stream kernel: 1 = the last workgroup finalises the step
     unsigned long long* stamps;     // diagnostic build only (PSGLA_STAMPS): per-wave work/wait cycles
 };
 
@@ -468,15 +471,28 @@ __global__ void __launch_bounds__(TV_THREADS) tv_finalise_kernel(const TvArgs a)
     const int P = a.B * a.C;
     const int T = a.tiles;
     const int G = a.per_chain_norm ? a.B : 1;
+#ifdef FIN_EMPTY
+    if (a.B > 0) return;
+#endif
     if (threadIdx.x == 0) s_flag = 0;
     __syncthreads();
     for (int g = threadIdx.x; g < G; g += blockDim.x) {
+        // all partial norms of the chain in flight at once (one memory latency, not n_tv)
+        double nd[MAXIT], nn[MAXIT];
+#pragma unroll
+        for (int t = 2; t < MAXIT; ++t) {
+            if (t <= a.n_tv - 2) {
+                nd[t] = a.norms[((size_t)g * a.n_tv + t) * 2];
+                nn[t] = a.norms[((size_t)g * a.n_tv + t) * 2 + 1];
+            }
+        }
         int stop = a.n_tv;
-        for (int t = 2; t <= a.n_tv - 2; ++t) {
-            const double nd = a.norms[((size_t)g * a.n_tv + t) * 2];
-            const double nn = a.norms[((size_t)g * a.n_tv + t) * 2 + 1];
-            const float rel = (float)sqrt(nd) / (float)sqrt(nn);
-            if (rel < a.tol) { stop = t + 1; break; }
+#pragma unroll
+        for (int t = 2; t < MAXIT; ++t) {
+            if (t <= a.n_tv - 2 && stop == a.n_tv) {
+                const float rel = (float)sqrt(nd[t]) / (float)sqrt(nn[t]);
+                if (rel < a.tol) stop = t + 1;
+            }
         }
         s_stop[g] = stop;
         if (stop < a.n_tv) atomicOr(&s_flag, 1);
@@ -491,7 +507,9 @@ __global__ void __launch_bounds__(TV_THREADS) tv_finalise_kernel(const TvArgs a)
     }
     __syncthreads();
     if (threadIdx.x == 0) {
+#ifndef FIN_NOFENCE
         __threadfence();
+#endif
         const int old = atomicAdd(a.arrive, 1);
         s_flag = (old == (int)gridDim.x - 1) ? 2 : 0;
     }
@@ -584,6 +602,15 @@ __device__ __forceinline__ void wait_vm_le(int n) {
     }
 }
 __device__ __forceinline__ void wait_vm_n(int n) { wait_vm_le<0>(n); }
+// 16-B store with sc1: the line leaves the XCD's L2 instead of staying dirty there, so the
+// end-of-pass agent release (buffer_wbl2) has almost nothing to write back.
+typedef float v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_sc1(float* p, const float4& v) {
+    const v4f x = {v.x, v.y, v.z, v.w};
+    // s_nop: the compiler does not see this store, so it cannot pad the store-data hazard
+    // (a VALU write of the data VGPRs right after a >8-byte store) -- the asm does
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
+}
 
 // Diagnostic build (-DPSGLA_STAMPS): every wave accumulates the cycles it spends working
 // between two pipeline barriers and the cycles it waits at them (s_memtime, shader clock).
@@ -678,7 +705,7 @@ __device__ __forceinline__ void build_rowmap(const TvArgs& a, int wg, RowMap& m)
     if (a.split_wgs <= 0) {
         m.ns = 1; m.Q = H; m.htop = 0; m.hbot = 0;
         m.q1 = m.q2 = m.q3 = H;
-        m.pl0 = wg / a.nsegs;
+        m.pl0 = wg / a.st_nsegs;
         return;
     }
     const long long T = (long long)a.B * a.C * H;
@@ -709,6 +736,14 @@ __device__ __forceinline__ void build_rowmap(const TvArgs& a, int wg, RowMap& m)
     if (m.ns <= 1) m.q1 = q;
     if (m.ns <= 2) m.q2 = q;
     if (m.ns <= 3) m.q3 = q;
+}
+
+// One whole plane (the early-stop recompute pass).
+__device__ __forceinline__ void plane_rowmap(int H, int plane, RowMap& m) {
+    m.ns = 1; m.Q = H; m.htop = 0; m.hbot = 0;
+    m.q1 = m.q2 = m.q3 = H;
+    m.pl0 = plane; m.pl1 = m.pl2 = m.pl3 = 0;
+    m.lo0 = m.lo1 = m.lo2 = m.lo3 = 0;
 }
 
 // Position of a role's current row in the stream; advanced monotonically (the segment walk
@@ -761,8 +796,9 @@ __device__ __forceinline__ void stage_phase_a(const TvArgs& a, const float4& X2,
 #pragma unroll
     for (int kk = 0; kk < CPL; ++kk) {
         const float u1left = kk > 0 ? o.u1[kk - 1] : u1l;
-        // nabla^T u2 in deepinv's order: (((0 - u0) + u0[i-1]) - u1) + u1[j-1]
-        const float tt = (((0.0f - o.u0[kk]) + pu0[kk]) - o.u1[kk]) + u1left;
+        // nabla^T u2 in deepinv's order: (((0 - u0) + u0[i-1]) - u1) + u1[j-1]; 0 - u0 + p == p - u0
+        // exactly (up to the sign of a zero, which no later operation can observe)
+        const float tt = ((pu0[kk] - o.u0[kk]) - o.u1[kk]) + u1left;
         const float xo = x2o[kk];
         float xv, zv, xn;
         if (EXACT) {
@@ -775,10 +811,19 @@ __device__ __forceinline__ void stage_phase_a(const TvArgs& a, const float4& X2,
             xn = __builtin_fmaf(a.rho, xv - xo, xo);
         }
         if (TRK) {
-            const float d = xo - xn;
-            const float q = xn + 1e-12f;
-            sd = __builtin_fmaf(d, d, sd);
-            sn = __builtin_fmaf(q, q, sn);
+            if (EXACT) {
+                const float d = xo - xn;
+                const float q = xn + 1e-12f;
+                sd = __builtin_fmaf(d, d, sd);
+                sn = __builtin_fmaf(q, q, sn);
+            } else {
+                // ||x2_prev - x2|| = rho ||x - x2_prev||: accumulate (x - x2_prev)^2, scaled by rho^2
+                // when the sums are published; the +1e-12 of ||x2 + 1e-12|| is below fp32 resolution
+                // of any pixel value that contributes
+                const float d = xv - xo;
+                sd = __builtin_fmaf(d, d, sd);
+                sn = __builtin_fmaf(xn, xn, sn);
+            }
         }
         o.z[kk] = zv;
         o.x2n[kk] = xn;
@@ -795,8 +840,9 @@ __device__ __forceinline__ void stage_phase_b(const TvArgs& a, const StageRow& r
     for (int kk = 0; kk < CPL; ++kk) {
         const float zc = ri.z[kk];
         const float zr = kk < CPL - 1 ? ri.z[kk + 1] : zr3;
-        const float g0 = DN ? ((0.0f - zc) + zj[kk]) : 0.0f;
-        float g1 = (0.0f - zc) + zr;
+        // deepinv: (0 - z) + z_next == z_next - z exactly (up to the sign of a zero)
+        const float g0 = DN ? (zj[kk] - zc) : 0.0f;
+        float g1 = zr - zc;
         if (kk == CPL - 1) g1 = last3 ? 0.0f : g1;
         const float uo0 = ri.u0[kk], uo1 = ri.u1[kk];
         if (EXACT) {
@@ -841,8 +887,9 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
     const int qc0 = rm.htop, qc1 = Q - rm.hbot;   // core stream rows
     auto flush = [&]() {
         if (TRK) {
-            const float d = wave_sum(core ? lsd : 0.f);
+            float d = wave_sum(core ? lsd : 0.f);
             const float q = wave_sum(core ? lsn : 0.f);
+            if (!EXACT) d *= a.rho * a.rho;          // fast sums hold (x - x2_prev)^2
             if (lane == 0) { sh.red[sacc][k - 1][0] = d; sh.red[sacc][k - 1][1] = q; }
             lsd = 0.f; lsn = 0.f;
         }
@@ -933,42 +980,35 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
     flush();
 }
 
+// One pass of the row-streaming pipeline over the rows of `rm` with n inner TV iterations
+// (front / stage / back roles, one barrier per step).  Inlined at two call sites: the main
+// pass and the rare early-stop recompute, each with its own register allocation.
 template <bool EXACT, bool ALPHA1>
-__global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
-    __shared__ StreamShared sh;
+__device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, const RowMap& rm, const int n,
+                                            const int cseg, const bool track, const long long step,
+                                            const bool fresh, Stamps& stp) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (scalar branches)
-    const int n = a.n_tv;
     const int H = a.H, W = a.W, C = a.C;
-    const long long step = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
-    const bool fresh = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
-    RowMap rm;
-    build_rowmap(a, blockIdx.x, rm);
-    const int Q = rm.Q;
-    const int qc0 = rm.htop, qc1 = Q - rm.hbot;          // core stream rows
-    const int cseg = a.split_wgs > 0 ? 0 : blockIdx.x - (blockIdx.x / a.nsegs) * a.nsegs;
-    const int cc0 = cseg * a.seg_w, cc1 = min(W, cc0 + a.seg_w);
-    const int f0 = max(0, cc0 - a.halo) & ~3;
-    const int gj0 = f0 + CPL * lane;
-    const bool lane_ok = gj0 < W;
-    const bool core = lane_ok && gj0 >= cc0 && gj0 < cc1;   // W % 4 == 0: a lane's 4 columns are all core or none
     const size_t HW = (size_t)H * W;
     const size_t E = (size_t)C * HW;
     const size_t BE = (size_t)a.B * E;
     const int par_in = (int)(step & 1), par_out = (int)((step + 1) & 1);
-    const int nsteps = Q + 4 + 3 * n;
-    const int role = (w < SP_FRONT) ? 0 : (w < SP_FRONT + n ? 1 : 2);
     const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    Stamps stp;
-    stp.t0 = stamp_now();
-#ifdef PSGLA_STAMPS
-    stp.w = w;
-    stp.tr = (a.stamps && blockIdx.x == 0) ? a.stamps + (size_t)gridDim.x * 32 : nullptr;
-#endif
     auto plane_off = [&](int pl) -> size_t { return (size_t)pl * HW; };   // planes are (b, c) in NCHW order
+    const int Q = rm.Q;
+    const int qc0 = rm.htop, qc1 = Q - rm.hbot;          // core stream rows
+    const int cc0 = cseg * a.st_seg_w, cc1 = min(W, cc0 + a.st_seg_w);
+    const int f0 = max(0, cc0 - a.st_halo) & ~3;
+    const int gj0 = f0 + CPL * lane;
+    const bool lane_ok = gj0 < W;
+    const bool core = lane_ok && gj0 >= cc0 && gj0 < cc1;   // W % 4 == 0: a lane's 4 columns are all core or none
+    const int nsteps = Q + 4 + 3 * n;
+    // 16 waves always; waves beyond the pipeline (n < 10) only keep the barrier count
+    const int role = (w < SP_FRONT) ? 0 : (w < SP_FRONT + n ? 1 : (w < SP_FRONT + n + SP_BACK ? 2 : 3));
 
     const int k_st = w - SP_FRONT + 1;                 // inner TV iteration (1-based)
-    const bool trk = role == 1 && (k_st - 1) >= 2 && (k_st - 1) <= n - 2;
+    const bool trk = track && role == 1 && (k_st - 1) >= 2 && (k_st - 1) <= n - 2;
     // Each role runs its own loop (its state is live only there); every wave executes
     // exactly nsteps barriers, so the s_barrier instances pair up across roles.
     if (role == 0) {
@@ -1034,8 +1074,13 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
                         float Yv[CPL];
 #pragma unroll
                         for (int k = 0; k < CPL; ++k) {
-                            const float g = (-mk[k] * (X[k] - yo[k])) / a.sigma2;
-                            Yv[k] = lane_ok ? (X[k] + a.c1 * g) + a.c2 * Z[k] : 0.f;
+                            if (EXACT) {
+                                const float g = (-mk[k] * (X[k] - yo[k])) / a.sigma2;
+                                Yv[k] = lane_ok ? (X[k] + a.c1 * g) + a.c2 * Z[k] : 0.f;
+                            } else {
+                                const float g = (mk[k] * (yo[k] - X[k])) * a.inv_sigma2;
+                                Yv[k] = lane_ok ? __builtin_fmaf(a.c2, Z[k], __builtin_fmaf(a.c1, g, X[k])) : 0.f;
+                            }
                         }
                         const float4 Y4 = make_float4(Yv[0], Yv[1], Yv[2], Yv[3]);
                         float4 x2s;
@@ -1066,6 +1111,8 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
         const bool last3 = gj0 + CPL - 1 == W - 1;
         if (trk) stage_loop<EXACT, true>(a, sh, rm, k_st, nsteps, lane, last3, core, stp);
         else stage_loop<EXACT, false>(a, sh, rm, k_st, nsteps, lane, last3, core, stp);
+    } else if (role == 3) {
+        for (int t = 0; t < nsteps; ++t) step_barrier(stp);
     } else {
         // ---------------- BACK state ----------------
         const int bw = w - SP_FRONT - n;                   // back wave id (stream rows q % 2 == bw)
@@ -1144,21 +1191,21 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
                     pend = rowcore ? nst : 0;
                     if (rowcore && core) {
                         const size_t base = plane_off(rc.p) + (size_t)rc.r * W + gj0;
-                        *reinterpret_cast<float4*>(a.x[par_out] + base) = Xo;
+                        st_sc1(a.x[par_out] + base, Xo);
                         float* u2o = a.u2[par_out] + 2 * base;
-                        *reinterpret_cast<float4*>(u2o) = make_float4(U0.x, U1.x, U0.y, U1.y);
-                        *reinterpret_cast<float4*>(u2o + 4) = make_float4(U0.z, U1.z, U0.w, U1.w);
-                        if (!ALPHA1) *reinterpret_cast<float4*>(a.x2[par_out] + base) = X2;
+                        st_sc1(u2o, make_float4(U0.x, U1.x, U0.y, U1.y));
+                        st_sc1(u2o + 4, make_float4(U0.z, U1.z, U0.w, U1.w));
+                        if (!ALPHA1) st_sc1(a.x2[par_out] + base, X2);
                         if (si.acc) {
                             if (si.blockend) {
-                                *reinterpret_cast<float4*>(a.blocks + (size_t)si.blk * BE + base) = M4;
-                                *reinterpret_cast<float4*>(a.blocks2 + (size_t)si.blk * BE + base) = Q4;
+                                st_sc1(a.blocks + (size_t)si.blk * BE + base, M4);
+                                st_sc1(a.blocks2 + (size_t)si.blk * BE + base, Q4);
                             } else if (si.liveout) {
-                                *reinterpret_cast<float4*>(a.mean[par_out] + base) = M4;
-                                *reinterpret_cast<float4*>(a.sq[par_out] + base) = Q4;
+                                st_sc1(a.mean[par_out] + base, M4);
+                                st_sc1(a.sq[par_out] + base, Q4);
                             }
                         }
-                        if (si.sample) *reinterpret_cast<float4*>(a.samples + (size_t)si.sidx * BE + base) = Xo;
+                        if (si.sample) st_sc1(a.samples + (size_t)si.sidx * BE + base, Xo);
                     }
                 }
             step_barrier(stp);
@@ -1177,15 +1224,107 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
 #endif
     // rel_err partial sums of this stream -> global, per segment's chain (deepinv's
     // early-stop test, per chain); the tracking stages wrote sh.red[segment][k - 1]
-    lds_barrier();
-    for (int tt = threadIdx.x; tt < SP_MAXSEG * SP_MAXST; tt += blockDim.x) {
-        const int sg = tt / SP_MAXST, it = tt - sg * SP_MAXST;     // it = k - 1
-        if (sg < rm.ns && it >= 2 && it <= n - 2) {
-            const int pl = rm.pl(sg);
-            const int g = a.per_chain_norm ? pl / C : 0;
-            atomicAdd(&a.norms[((size_t)g * a.n_tv + it) * 2], (double)sh.red[sg][it][0]);
-            atomicAdd(&a.norms[((size_t)g * a.n_tv + it) * 2 + 1], (double)sh.red[sg][it][1]);
+}
+
+template <bool EXACT, bool ALPHA1>
+__global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
+    __shared__ StreamShared sh;
+    __shared__ int s_stop[MAXG];
+    __shared__ int s_flag, s_item, s_next;
+    const int C = a.C;
+    const long long step = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
+    const bool fresh = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
+    Stamps stp;
+    stp.t0 = stamp_now();
+#ifdef PSGLA_STAMPS
+    stp.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    stp.tr = (a.stamps && blockIdx.x == 0) ? a.stamps + (size_t)gridDim.x * 32 : nullptr;
+#endif
+    {
+        RowMap rm;
+        build_rowmap(a, blockIdx.x, rm);
+        const int cseg = a.split_wgs > 0 ? 0 : blockIdx.x - (blockIdx.x / a.st_nsegs) * a.st_nsegs;
+        stream_pass<EXACT, ALPHA1>(a, sh, rm, a.n_tv, cseg, true, step, fresh, stp);
+        if (!a.fin_inline) return;        // main-pass-only launch (kernel timing): no side effects
+        // rel_err partial sums of this stream -> global, per segment's chain (deepinv's
+        // early-stop test, per chain); the tracking stages wrote sh.red[segment][k - 1]
+        lds_barrier();
+        for (int tt = threadIdx.x; tt < SP_MAXSEG * SP_MAXST; tt += blockDim.x) {
+            const int sg = tt / SP_MAXST, it = tt - sg * SP_MAXST;     // it = k - 1
+            if (sg < rm.ns && it >= 2 && it <= a.n_tv - 2) {
+                const int pl = rm.pl(sg);
+                const int g = a.per_chain_norm ? pl / C : 0;
+                atomicAdd(&a.norms[((size_t)g * a.n_tv + it) * 2], (double)sh.red[sg][it][0]);
+                atomicAdd(&a.norms[((size_t)g * a.n_tv + it) * 2 + 1], (double)sh.red[sg][it][1]);
+            }
         }
+    }
+    // ---- step finalisation by the last workgroup to arrive (no second launch) ----
+    // Every wave's stores and atomics complete, then one agent release per workgroup (cheap: the
+    // outputs were stored sc1 and are not dirty in L2), then the arrival count.  The last
+    // workgroup acquires before reading the rel-err sums or re-streaming a chain.
+    wait_vm0();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const int old = __hip_atomic_fetch_add(a.arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_flag = (old == (int)gridDim.x - 1) ? 1 : 0;
+        if (s_flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    wait_vm0();
+    __syncthreads();
+    if (!s_flag) return;
+    // deepinv's early stop per chain: rel_err < tol at inner iteration t >= 2 -> the chain
+    // stops after t + 1 iterations.  All (chain, t) tests in parallel: bit t of s_stop[g].
+    const int G = a.B;
+    for (int g = threadIdx.x; g < G; g += blockDim.x) s_stop[g] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < G * SP_MAXST; i += blockDim.x) {
+        const int g = i / SP_MAXST, t = i - g * SP_MAXST;
+        if (t >= 2 && t <= a.n_tv - 2) {
+            const double nd = a.norms[((size_t)g * a.n_tv + t) * 2];
+            const double nn = a.norms[((size_t)g * a.n_tv + t) * 2 + 1];
+            const float rel = (float)sqrt(nd) / (float)sqrt(nn);
+            if (rel < a.tol) atomicOr(&s_stop[g], 1 << t);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) { s_next = 0; s_item = 0; }
+    __syncthreads();
+    for (int g = threadIdx.x; g < G; g += blockDim.x) {
+        const int m = s_stop[g];
+        s_stop[g] = m ? (__ffs(m) - 1) + 1 : a.n_tv;
+        if (m) s_item = 1;                    // some chain stopped early (benign race: all write 1)
+    }
+    __syncthreads();
+    if (s_item == 0) s_next = 1 << 30;        // common case: nothing to redo, skip the scan
+    // rare: re-stream every (plane, column segment) of a stopped chain alone with the stopped
+    // iteration count (the step's inputs are intact: ping-pong state)
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int items = a.B * C * a.st_nsegs;
+            int it = min(s_next, items), found = -1;
+            for (; it < items; ++it)
+                if (s_stop[(it / a.st_nsegs) / C] < a.n_tv) { found = it; break; }
+            s_item = found;
+            s_next = it + 1;
+        }
+        __syncthreads();
+        const int item = __builtin_amdgcn_readfirstlane(s_item);
+        if (item < 0) break;
+        const int plane = item / a.st_nsegs;
+        RowMap rm;
+        plane_rowmap(a.H, plane, rm);
+        const int nstop = __builtin_amdgcn_readfirstlane(s_stop[plane / C]);
+        stream_pass<EXACT, ALPHA1>(a, sh, rm, nstop, item - plane * a.st_nsegs, false, step, fresh, stp);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.B * a.n_tv * 2; i += blockDim.x) a.norms[i] = 0.0;
+    if (threadIdx.x == 0) {
+        *a.arrive = 0;
+        if (a.fresh_dev) *a.fresh_dev = 0;
+        if (a.advance_step && a.d_step) *a.d_step = *a.d_step + 1;
     }
 }
 
@@ -1439,18 +1578,19 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
     if (mask & 1) {
         if (FRONT == FRONT_INPAINT && a.stream) {
             TvArgs s = a;
-            s.halo = a.n_tv;
-            s.nbands = 1;
-            s.band_h = a.H;
-            if (a.W <= TV_COLS) { s.seg_w = a.W; s.nsegs = 1; }
+            s.st_halo = a.n_tv;
+            if (a.W <= TV_COLS) { s.st_seg_w = a.W; s.st_nsegs = 1; }
             else {
-                const int sw = (TV_COLS - 2 * s.halo - 3) & ~3;
-                s.nsegs = (a.W + sw - 1) / sw;
-                s.seg_w = (((a.W + s.nsegs - 1) / s.nsegs) + 3) & ~3;
+                const int sw = (TV_COLS - 2 * s.st_halo - 3) & ~3;
+                s.st_nsegs = (a.W + sw - 1) / sw;
+                s.st_seg_w = (((a.W + s.st_nsegs - 1) / s.st_nsegs) + 3) & ~3;
             }
-            const int threads = WAVE * (SP_FRONT + a.n_tv + SP_BACK);
-            const int grid = s.split_wgs > 0 ? s.split_wgs : P * s.nsegs;
-            hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1>), dim3(grid), dim3(threads), 0, st, s);
+            s.fin_inline = (mask & 2) ? 1 : 0;
+            const int grid = s.split_wgs > 0 ? s.split_wgs : P * s.st_nsegs;
+            hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+            int rc = launch_check("tv_stream_kernel");
+            if (rc) return rc;
+            return 0;                    // finalised in-kernel (or main pass only)
         } else {
             const int grid_main = ((P + 7) / 8) * 8 * a.tiles;
             hipLaunchKernelGGL((tv_main_kernel<EXACT, FRONT, ALPHA1>), dim3(grid_main), dim3(TV_THREADS), 0, st, a);
@@ -1459,7 +1599,10 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
         if (rc) return rc;
     }
     if (!(mask & 2)) return 0;
-    const int grid_fin = (P * a.tiles < 256) ? P * a.tiles : 256;
+    // Few workgroups: every one re-derives the per-chain stop flags (cheap) and they meet on one
+    // arrival counter -- 8 contending atomics instead of one per CU (measured 13.5 us -> see
+    // DESIGN.md).  The rare early-stop recompute is spread over these workgroups.
+    const int grid_fin = (P * a.tiles < 8) ? P * a.tiles : 8;
     hipLaunchKernelGGL((tv_finalise_kernel<EXACT, FRONT, ALPHA1>), dim3(grid_fin), dim3(TV_THREADS), 0, st, a);
     return launch_check("tv_kernel(finalise)");
 }
@@ -1499,6 +1642,7 @@ int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream) {
     a.c1 = d->c1; a.c2 = d->c2; a.sigma2 = d->sigma2; a.alpha = d->alpha;
     a.tau = d->tau; a.opt = d->one_plus_tau; a.inv_opt = (float)(1.0 / (double)d->one_plus_tau);
     a.sig_tv = d->sigma_tv; a.rho = d->rho; a.ths = d->ths; a.tol = d->tol;
+    a.inv_sigma2 = (float)(1.0 / (double)a.sigma2);
     a.n_tv = d->n_tv; a.seed = d->seed; a.chain0 = d->chain0; a.pingpong = 1;
     a.d_step = (long long*)s->d_step; a.step_offset = s->step_offset;
     a.fresh_dev = d->fresh; a.per_chain_norm = 1; a.norms = d->norms; a.arrive = d->arrive;

@@ -236,6 +236,48 @@ def test_stream_row_split_exact_vs_oracle(stream_wgs):
         np.testing.assert_array_equal(eng.u2_state[b].cpu().numpy(), u2[0])
 
 
+class _RecordingTV(orc.TVDenoiser):
+    def __init__(self, **kw):
+        super().__init__(**kw)
+        self.its = []
+
+    def forward(self, y, ths):
+        out = super().forward(y, ths)
+        self.its.append(self.last_n_it)
+        return out
+
+
+@pytest.mark.parametrize("stream_wgs", [0, -1])
+def test_stream_early_stop_exact_vs_oracle(stream_wgs):
+    """tol large enough that deepinv's early stop fires in some steps: the stream kernel's last
+    workgroup re-streams the stopped chains' planes with k+1 iterations -- bit-identical."""
+    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    B, H, W, n_iter, tol = 2, 40, 52, 12, 3e-2
+    g = torch.Generator().manual_seed(7)
+    x = torch.rand((1, 3, H, W), generator=g)
+    dg, y, init, mask2d = orc.inpainting_problem(x, seed_ip=2)
+    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
+    eng = FusedTvChains(init.expand(B, -1, -1, -1).contiguous().to(DEV), y.to(DEV), mask2d.to(torch.uint8).to(DEV),
+                        c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)), alpha=1.0,
+                        ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10, tol=tol), seed=4,
+                        n_iter=n_iter, n_inter=3, n_inter_mmse=2, exact=True, kernel_variant="stream",
+                        stream_wgs=stream_wgs)
+    eng.run(n_iter, graph_steps=0)
+    torch.cuda.synchronize()
+    bm, bm2 = eng.blocks()
+    fired = False
+    for b in range(B):
+        tv = _RecordingTV(n_it_max=10, tol=tol)
+        Xl, Ml, M2l = orc.psgla(init, dg, tv, torch.tensor(1.0), torch.tensor(10.0), sig_float=10 / 255.0,
+                                delta=(10 / 255.0) ** 2, n_iter=n_iter, n_inter=3, n_inter_mmse=2, seed=4, chain=b)
+        fired = fired or min(tv.its) < 10
+        np.testing.assert_array_equal(eng.samples()[:, b].cpu().numpy(), np.stack([t.numpy() for t in Xl]))
+        np.testing.assert_array_equal(bm[:, b].cpu().numpy(), np.stack([t.numpy() for t in Ml]))
+        np.testing.assert_array_equal(eng.u2_state[b].cpu().numpy(), tv.u2.numpy()[0])
+    assert fired, "test needs the early stop to fire"
+
+
 def test_stream_row_split_rejects_bad_counts():
     from psgla_for_posterior_sampling_amd._native import NativeLibraryError
     for bad in (1, 10 ** 6):           # fewer than ceil(B*C/3) ranges / more ranges than rows
