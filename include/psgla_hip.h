@@ -162,6 +162,16 @@ int psgla_inpaint_grad(const float* X, const float* y, int64_t y_chain_stride, c
                        int64_t mask_chain_stride, float* g, int32_t B, int32_t C, int32_t H,
                        int32_t W, float sigma2, void* stream);
 
+/* Deblurring data term (sampling_images.py:329-338), circular (2l+1)^2 depthwise stencils:
+ *   g = -A^T(A X - y) / sigma2,  A = conv2d(pad(., l, circular), hconv),  A^T: same with hcorr
+ * hconv / hcorr: device [(2l+1)^2] taps (row-major, the same for every channel), l <= 8.
+ * With Y != NULL the Langevin update of restoration_algorithms.py:232-236 is fused:
+ *   Y = (X + c1 g) + c2 Z  (Z: the noise stream of psgla_langevin_update) and g is not written;
+ * else g is written.  exact = 1: multiply-then-add taps and IEEE division (else fma, 1/sigma2). */
+int psgla_blur_grad(const float* X, const float* y, int64_t y_chain_stride, const float* hconv, const float* hcorr,
+                    int32_t l, float* g, float* Y, int32_t B, int32_t C, int32_t H, int32_t W, float sigma2,
+                    float c1, float c2, uint64_t seed, int32_t chain0, const int64_t* d_step, int64_t step_offset,
+                    int32_t exact, void* stream);
 /* *d_step += 1 (one thread) */
 int psgla_advance_step(int64_t* d_step, void* stream);
 

@@ -1377,6 +1377,118 @@ __global__ void langevin_update_kernel(const float* X, const float* g, float* Y,
     }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Deblurring data term (sampling_images.py:304-341): g = -A^T(A x - y) / sigma2 with
+// A x = conv2d(pad(x, l, circular), hconv) and A^T r = conv2d(pad(r, l, circular), hcorr),
+// depthwise, K = 2l+1 taps per side.  One workgroup per 32 x 64 output tile of a plane:
+// x is staged in LDS with a 2l halo (circular wrap on load), r = A x - y is formed in LDS
+// on the tile + l halo, then A^T r; the taps sit in LDS and are read as broadcasts.
+// With Y != NULL the Langevin update Y = (X + c1 g) + c2 Z is fused (g is never stored).
+// ---------------------------------------------------------------------------------------
+constexpr int BL_TH = 32, BL_TW = 64, BL_MAXL = 8, BL_THREADS = 256;
+constexpr int BL_XH = BL_TH + 4 * BL_MAXL, BL_XW = BL_TW + 4 * BL_MAXL;
+constexpr int BL_RH = BL_TH + 2 * BL_MAXL, BL_RW = BL_TW + 2 * BL_MAXL;
+
+struct BlurArgs {
+    const float* X;
+    const float* y;
+    long long y_cs;
+    const float* hconv;
+    const float* hcorr;
+    int l;
+    float* g;
+    float* Y;
+    int B, C, H, W;
+    float sigma2, inv_sigma2, c1, c2;
+    unsigned long long seed;
+    int chain0;
+    const long long* d_step;
+    long long off;
+    int exact;
+    int tiles_x;
+};
+
+template <bool EXACT>
+__global__ void __launch_bounds__(BL_THREADS) blur_grad_kernel(const BlurArgs a) {
+    __shared__ float xs[BL_XH][BL_XW + 1];
+    __shared__ float rs[BL_RH][BL_RW + 1];
+    __shared__ float hc[(2 * BL_MAXL + 1) * (2 * BL_MAXL + 1)];
+    __shared__ float hr[(2 * BL_MAXL + 1) * (2 * BL_MAXL + 1)];
+    const int l = a.l, K = 2 * l + 1, H = a.H, W = a.W;
+    const int plane = blockIdx.y, b = plane / a.C, c = plane - b * a.C;
+    const int ty = blockIdx.x / a.tiles_x, tx = blockIdx.x - ty * a.tiles_x;
+    const int i0 = ty * BL_TH, j0 = tx * BL_TW;
+    const size_t HW = (size_t)H * W;
+    const float* xp = a.X + (size_t)plane * HW;
+    const float* yp = a.y + (size_t)b * a.y_cs + (size_t)c * HW;
+    for (int t = threadIdx.x; t < K * K; t += BL_THREADS) { hc[t] = a.hconv[t]; hr[t] = a.hcorr[t]; }
+    // x on rows i0-2l .. i0+TH+2l-1, cols j0-2l .. j0+TW+2l-1 (circular)
+    const int xh = BL_TH + 4 * l, xw = BL_TW + 4 * l;
+    for (int t = threadIdx.x; t < xh * xw; t += BL_THREADS) {
+        const int p = t / xw, q = t - p * xw;
+        int gi = (i0 - 2 * l + p) % H; if (gi < 0) gi += H;
+        int gj = (j0 - 2 * l + q) % W; if (gj < 0) gj += W;
+        xs[p][q] = xp[(size_t)gi * W + gj];
+    }
+    __syncthreads();
+    // r = A x - y on rows i0-l .. i0+TH+l-1 (tap order a, b row-major)
+    const int rh = BL_TH + 2 * l, rw = BL_TW + 2 * l;
+    for (int t = threadIdx.x; t < rh * rw; t += BL_THREADS) {
+        const int p = t / rw, q = t - p * rw;
+        float acc = 0.0f;
+        for (int u = 0; u < K; ++u)
+            for (int v = 0; v < K; ++v) {
+                if (EXACT) acc = acc + hc[u * K + v] * xs[p + u][q + v];
+                else acc = __builtin_fmaf(hc[u * K + v], xs[p + u][q + v], acc);
+            }
+        int gi = (i0 - l + p) % H; if (gi < 0) gi += H;
+        int gj = (j0 - l + q) % W; if (gj < 0) gj += W;
+        rs[p][q] = acc - yp[(size_t)gi * W + gj];
+    }
+    __syncthreads();
+    // g = -(A^T r) / sigma2 on the tile; a thread owns 4 consecutive columns x 2 rows
+    const long long step = (a.d_step ? *a.d_step : 0LL) + a.off;
+    const int tq = threadIdx.x & 15, tr = threadIdx.x >> 4;
+    for (int rr = 0; rr < 2; ++rr) {
+        const int p = tr * 2 + rr;
+        const int i = i0 + p;
+        if (i >= H) continue;
+        float gv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int q = tq * 4 + k;
+            float acc = 0.0f;
+            for (int u = 0; u < K; ++u)
+                for (int v = 0; v < K; ++v) {
+                    if (EXACT) acc = acc + hr[u * K + v] * rs[p + u][q + v];
+                    else acc = __builtin_fmaf(hr[u * K + v], rs[p + u][q + v], acc);
+                }
+            gv[k] = EXACT ? (-acc) / a.sigma2 : (-acc) * a.inv_sigma2;
+        }
+        const int j = j0 + tq * 4;
+        const size_t e0 = (size_t)c * HW + (size_t)i * W + j;   // element index within the chain
+        const size_t o = (size_t)b * a.C * HW + e0;
+        if (a.Y) {
+            float z[4];
+            if ((W & 3) == 0) {
+                normal_quad(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)(e0 >> 2), z);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    z[k] = normal_elem(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint64_t)(e0 + k));
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (j + k < W) a.Y[o + k] = (a.X[o + k] + a.c1 * gv[k]) + a.c2 * z[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (j + k < W) a.g[o + k] = gv[k];
+        }
+    }
+}
+
 struct AccArgs {
     int n_inter, nm;
     const float* coef;
@@ -1710,6 +1822,27 @@ int psgla_langevin_update(const float* X, const float* g, float* Y, int32_t B, i
                        g, Y, B, (long long)E, c1, c2, (unsigned long long)seed, chain0,
                        (const long long*)d_step, (long long)step_offset);
     return launch_check("langevin_update");
+}
+
+int psgla_blur_grad(const float* X, const float* y, int64_t y_chain_stride, const float* hconv, const float* hcorr,
+                    int32_t l, float* g, float* Y, int32_t B, int32_t C, int32_t H, int32_t W, float sigma2,
+                    float c1, float c2, uint64_t seed, int32_t chain0, const int64_t* d_step, int64_t step_offset,
+                    int32_t exact, void* stream) {
+    if (!X || !y || !hconv || !hcorr || (!g && !Y) || B <= 0 || C <= 0 || H <= 0 || W <= 0)
+        return fail(0, "psgla_blur_grad: bad arguments");
+    if (l < 0 || l > BL_MAXL) return fail(0, "psgla_blur_grad: blur half-width l outside [0, 8]");
+    if ((long long)B * C > 65535) return fail(0, "psgla_blur_grad: more than 65535 planes in one launch");
+    BlurArgs a;
+    a.X = X; a.y = y; a.y_cs = y_chain_stride; a.hconv = hconv; a.hcorr = hcorr; a.l = l; a.g = g; a.Y = Y;
+    a.B = B; a.C = C; a.H = H; a.W = W; a.sigma2 = sigma2; a.inv_sigma2 = (float)(1.0 / (double)sigma2);
+    a.c1 = c1; a.c2 = c2; a.seed = seed; a.chain0 = chain0; a.d_step = (const long long*)d_step;
+    a.off = step_offset; a.exact = exact;
+    a.tiles_x = (W + BL_TW - 1) / BL_TW;
+    const int tiles_y = (H + BL_TH - 1) / BL_TH;
+    const dim3 grid(a.tiles_x * tiles_y, B * C);
+    if (exact) hipLaunchKernelGGL(blur_grad_kernel<true>, grid, dim3(BL_THREADS), 0, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL(blur_grad_kernel<false>, grid, dim3(BL_THREADS), 0, (hipStream_t)stream, a);
+    return launch_check("blur_grad");
 }
 
 static AccArgs make_acc(const PsglaSchedule* s) {

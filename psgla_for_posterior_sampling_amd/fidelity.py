@@ -64,13 +64,24 @@ def blur_kernel(l: int = 4, blur_type: str = "uniform", si: float = 1.0) -> np.n
 
 class BlurFidelity:
     """g(x) = -A^T(A x - y) / sigma2 with A = circular (2l+1)^2 depthwise convolution
-    (sampling_images.py:329-338).  Evaluated with the same torch conv2d calls as the reference
-    (the HIP deblurring step kernel is DESIGN.md's next item)."""
+    (sampling_images.py:329-338).  Calling it runs the HIP stencil kernel (psgla_blur_grad);
+    psgla() fuses it with the Langevin update.  A / AT (torch conv2d, as the reference) are kept
+    for the one-time observation synthesis y = A(x) + noise."""
 
-    def __init__(self, hconv: torch.Tensor, hcorr: torch.Tensor, l: int, y: torch.Tensor, sigma2):
+    def __init__(self, hconv: torch.Tensor, hcorr: torch.Tensor, l: int, y: torch.Tensor | None, sigma2,
+                 exact: bool = False):
         self.hconv, self.hcorr, self.l = hconv, hcorr, int(l)
         self.y = y
-        self.sigma2t = torch.as_tensor(sigma2, dtype=torch.float32, device=y.device)
+        self.sigma2t = torch.as_tensor(sigma2, dtype=torch.float32, device=hconv.device)
+        self.sigma2 = float(self.sigma2t.item())
+        self.exact = exact
+        # the HIP kernel takes one (2l+1, 2l+1) tap set shared by all channels
+        hc = hconv.reshape(-1, hconv.shape[-2], hconv.shape[-1])
+        hr = hcorr.reshape(-1, hcorr.shape[-2], hcorr.shape[-1])
+        if not (torch.equal(hc, hc[:1].expand_as(hc)) and torch.equal(hr, hr[:1].expand_as(hr))):
+            raise ValueError("BlurFidelity: per-channel blur kernels must be identical")
+        self.taps_conv = hc[0].contiguous().float()
+        self.taps_corr = hr[0].contiguous().float()
 
     def A(self, x):
         l = self.l
@@ -83,7 +94,8 @@ class BlurFidelity:
                                           self.hcorr, groups=x.size(1), padding=0)
 
     def __call__(self, x):
-        return -self.AT(self.A(x) - self.y) / self.sigma2t
+        return K.blur_grad(x.contiguous(), self.y.contiguous(), self.taps_conv, self.taps_corr, self.l, self.sigma2,
+                           exact=self.exact)
 
 
 def deblurring_problem(im_t: torch.Tensor, seed_ip: int = 0, l: int = 4, blur_type: str = "uniform",

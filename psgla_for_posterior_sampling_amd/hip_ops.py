@@ -152,6 +152,34 @@ def inpaint_grad(X, y, mask_u8, sigma2: float, out=None):
     return out
 
 
+def blur_grad(X, y, hconv, hcorr, l: int, sigma2: float, out=None, exact: bool = False):
+    """g = -A^T(A X - y) / sigma2 (circular depthwise (2l+1)^2 stencils, sampling_images.py:329-338).
+    hconv / hcorr: (2l+1, 2l+1) fp32 device taps shared by every channel."""
+    B, C, H, W = X.shape
+    if out is None:
+        out = torch.empty_like(X)
+    y_cs = 0 if y.shape[0] == 1 else C * H * W
+    N.check(N.lib().psgla_blur_grad(_ptr(X, name="X"), _ptr(y, name="y"), y_cs, _ptr(hconv, name="hconv"),
+                                    _ptr(hcorr, name="hcorr"), int(l), _ptr(out, name="g"), None, B, C, H, W,
+                                    sigma2, 0.0, 0.0, 0, 0, None, 0, int(exact), _stream()), "psgla_blur_grad")
+    return out
+
+
+def blur_langevin(X, y, hconv, hcorr, l: int, sigma2: float, c1: float, c2: float, seed: int, chain0: int,
+                  step: int, out=None, exact: bool = False, d_step: torch.Tensor | None = None):
+    """Y = (X + c1 g(X)) + c2 Z with the deblurring g fused (restoration_algorithms.py:232-236)."""
+    B, C, H, W = X.shape
+    if out is None:
+        out = torch.empty_like(X)
+    y_cs = 0 if y.shape[0] == 1 else C * H * W
+    N.check(N.lib().psgla_blur_grad(_ptr(X, name="X"), _ptr(y, name="y"), y_cs, _ptr(hconv, name="hconv"),
+                                    _ptr(hcorr, name="hcorr"), int(l), None, _ptr(out, name="Y"), B, C, H, W,
+                                    sigma2, c1, c2, seed & (2 ** 64 - 1), chain0,
+                                    d_step.data_ptr() if d_step is not None else None, step, int(exact),
+                                    _stream()), "psgla_blur_grad")
+    return out
+
+
 def advance_step(d_step: torch.Tensor):
     N.check(N.lib().psgla_advance_step(_ptr(d_step, torch.int64, "d_step"), _stream()), "psgla_advance_step")
 

@@ -10,7 +10,8 @@ Dispatch:
   the fused HIP step (one kernel launch per Langevin step, hipGraph-replayed): config 2.
 * anything else (opaque closures, torch denoisers) -> the closures are called as given,
   and the rest of the step (Gaussian noise, Langevin update, relaxation, accumulators,
-  sample storage) runs as HIP kernels.
+  sample storage) runs as HIP kernels; a ``BlurFidelity`` data term is fused with the
+  Langevin update (one stencil kernel).
 The Gaussian noise is the in-kernel "psgla noise v1" stream of (seed, chain) instead of
 torch's generator (whose CUDA stream depends on the device's CU count); extra keyword
 ``chain0`` gives the global id of the first chain when a batch is sharded over GPUs.
@@ -28,7 +29,7 @@ import torch
 from . import hip_ops as K
 from .denoisers import TVDenoiser
 from .engine import FusedTvChains
-from .fidelity import InpaintingFidelity
+from .fidelity import BlurFidelity, InpaintingFidelity
 
 DEFAULT_GRAPH_STEPS = int(os.environ.get("PSGLA_GRAPH_STEPS", "50"))
 
@@ -120,9 +121,14 @@ def psgla(init, data_grad, denoiser, alpha, lambd, sig_float=0.0055, delta=4e-5,
     sq = torch.zeros_like(X)
     sig_den = torch.tensor(sig_noised).to(dev).to(torch.float32)
     with torch.no_grad():
+        blur = isinstance(data_grad, BlurFidelity)
         for i in range(n_iter):
-            g = data_grad(X)
-            K.langevin_update(X, g.contiguous().float(), c1, c2, seed, chain0, i, out=Y)
+            if blur:    # deblurring: gradient stencil and Langevin update in one HIP kernel
+                K.blur_langevin(X, data_grad.y.contiguous(), data_grad.taps_conv, data_grad.taps_corr, data_grad.l,
+                                data_grad.sigma2, c1, c2, seed, chain0, i, out=Y, exact=data_grad.exact)
+            else:
+                g = data_grad(X)
+                K.langevin_update(X, g.contiguous().float(), c1, c2, seed, chain0, i, out=Y)
             D = denoiser.forward(Y, sig_den)
             K.relax_accumulate(Y, D.contiguous(), Xn, alpha_f, mean, sq, sched, i)
             X, Xn = Xn, X

@@ -397,3 +397,83 @@ def test_inpaint_grad_bitwise():
     dg = InpaintingFidelity(mask2d.to(DEV), y.to(DEV), torch.tensor((1 / 255.0) ** 2, dtype=torch.float32))
     x = torch.rand(init.shape)
     np.testing.assert_array_equal(dg(x.to(DEV)).cpu().numpy(), dg_ref(x).numpy())
+
+
+# ---------------------------------------------------------------------------------------
+# Deblurring data term (HIP stencil) -- sampling_images.py:304-341
+# ---------------------------------------------------------------------------------------
+def _blur_case(B, H, W, l, bt, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand((B, 3, H, W), generator=g)
+    A, AT = orc.blur_operators(l=l, blur_type=bt)
+    y = A(x) + torch.normal(torch.zeros_like(x), (1 / 255.0) * torch.ones_like(x), generator=g)
+    xs = (x + 0.05 * torch.randn(x.shape, generator=g)).contiguous()
+    s2 = torch.tensor((1 / 255.0) ** 2, dtype=torch.float32)
+    ref = -AT(A(xs) - y) / s2           # the reference's closure, torch CPU
+    return xs, y, ref
+
+
+# the stencil sums 2 x 81 products in its own order (torch's CPU conv2d order is not specified),
+# so parity is a tolerance: |g - g_ref| <= BLUR_TOL * max|g_ref|; A x - y cancels to the noise
+# level, which amplifies fp32 rounding of the 81-term sums by ~100x relative to |g|.
+BLUR_TOL = 2e-5
+
+
+@pytest.mark.parametrize("B,H,W,l,bt", [(2, 40, 52, 4, "uniform"), (1, 37, 29, 4, "gaussian"),
+                                        (2, 70, 130, 2, "uniform"), (1, 16, 16, 0, "uniform")])
+@pytest.mark.parametrize("exact", [True, False])
+def test_blur_grad_matches_reference_closure(B, H, W, l, bt, exact):
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    xs, y, ref = _blur_case(B, H, W, l, bt, seed=B * H + W)
+    h_ = orc.blur_kernel(l, bt)
+    hconv = torch.from_numpy(np.copy(np.flip(h_))).float().to(DEV)
+    hcorr = torch.from_numpy(h_).float().to(DEV)
+    g = K.blur_grad(xs.to(DEV), y.to(DEV), hconv, hcorr, l, float(np.float32((1 / 255.0) ** 2)), exact=exact)
+    torch.cuda.synchronize()
+    err = (g.cpu() - ref).abs().max().item()
+    assert err <= BLUR_TOL * ref.abs().max().item(), err
+
+
+def test_blur_langevin_fused_equals_grad_then_update():
+    """The fused stencil + Langevin kernel == blur_grad followed by langevin_update (same noise)."""
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    xs, y, _ = _blur_case(2, 40, 52, 4, "uniform", seed=3)
+    h_ = orc.blur_kernel(4, "uniform")
+    hconv = torch.from_numpy(np.copy(np.flip(h_))).float().to(DEV)
+    hcorr = torch.from_numpy(h_).float().to(DEV)
+    X, yd = xs.to(DEV), y.to(DEV)
+    s2 = float(np.float32((1 / 255.0) ** 2))
+    for W in (52, 30):                                  # quad-aligned and per-element noise paths
+        Xw, yw = X[..., :W].contiguous(), yd[..., :W].contiguous()
+        g = K.blur_grad(Xw, yw, hconv, hcorr, 4, s2, exact=True)
+        Y1 = K.langevin_update(Xw, g, 1e-4, 0.05, seed=9, chain0=3, step=17)
+        Y2 = K.blur_langevin(Xw, yw, hconv, hcorr, 4, s2, 1e-4, 0.05, seed=9, chain0=3, step=17, exact=True)
+        torch.cuda.synchronize()
+        assert torch.equal(Y1, Y2)
+
+
+@pytest.mark.parametrize("bt", ["uniform", "gaussian"])
+def test_generic_psgla_deblur_matches_reference_fixture(bt):
+    """psgla with the HIP deblurring step (fused stencil + Langevin) vs the reference's own run
+    (tests/golden psgla_deblur_*: clamp denoiser, 60 steps): sample means within REL_TOL_MEAN."""
+    from psgla_for_posterior_sampling_amd import restoration_algorithms as RA
+    from psgla_for_posterior_sampling_amd.fidelity import BlurFidelity
+    fx = load(f"psgla_deblur_{bt}")
+    seed, n, ni, nm, alpha, lam, s, delta, l = fx["meta"]
+    l = int(l)
+    hcorr = torch.from_numpy(fx["hcorr"]).float()
+    hconv = torch.flip(hcorr, dims=(0, 1)).contiguous()
+    ones = torch.ones(3, 2 * l + 1, 2 * l + 1)
+    dg = BlurFidelity((hconv[None, None] * ones[:, None]).to(DEV), (hcorr[None, None] * ones[:, None]).to(DEV), l,
+                      torch.from_numpy(fx["y"]).to(DEV), torch.tensor((1 / 255.0) ** 2, dtype=torch.float32))
+
+    class Clamp:
+        def forward(self, x, s):
+            return torch.clamp(x, 0.0, 1.0)
+    out = RA.psgla(torch.from_numpy(fx["init"]).to(DEV), dg, Clamp(), torch.tensor(alpha, dtype=torch.float32),
+                   torch.tensor(lam, dtype=torch.float32), sig_float=float(s), delta=float(delta),
+                   n_iter=int(n), n_inter=int(ni), n_inter_mmse=int(nm), seed=int(seed))
+    Xl, Ml, M2l = [np.stack([t.cpu().numpy() for t in lst]) for lst in out]
+    assert Xl.shape == fx["samples"].shape and Ml.shape == fx["blocks"].shape
+    assert rel(Ml.mean(0), fx["blocks"].mean(0)) < REL_TOL_MEAN
+    assert rel(M2l.mean(0), fx["blocks2"].mean(0)) < REL_TOL_MEAN
