@@ -164,7 +164,8 @@ int psgla_inpaint_grad(const float* X, const float* y, int64_t y_chain_stride, c
 
 /* Deblurring data term (sampling_images.py:329-338), circular (2l+1)^2 depthwise stencils:
  *   g = -A^T(A X - y) / sigma2,  A = conv2d(pad(., l, circular), hconv),  A^T: same with hcorr
- * hconv / hcorr: device [(2l+1)^2] taps (row-major, the same for every channel), l <= 8.
+ * hconv / hcorr: HOST arrays of (2l+1)^2 fp32 taps (row-major, the same for every channel;
+ *   copied into the launch's arguments), l <= 8.  X, y, g, Y: device.
  * With Y != NULL the Langevin update of restoration_algorithms.py:232-236 is fused:
  *   Y = (X + c1 g) + c2 Z  (Z: the noise stream of psgla_langevin_update) and g is not written;
  * else g is written.  exact = 1: multiply-then-add taps and IEEE division (else fma, 1/sigma2). */

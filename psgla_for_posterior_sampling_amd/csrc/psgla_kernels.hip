@@ -1381,22 +1381,22 @@ __global__ void langevin_update_kernel(const float* X, const float* g, float* Y,
 // ---------------------------------------------------------------------------------------
 // Deblurring data term (sampling_images.py:304-341): g = -A^T(A x - y) / sigma2 with
 // A x = conv2d(pad(x, l, circular), hconv) and A^T r = conv2d(pad(r, l, circular), hcorr),
-// depthwise, K = 2l+1 taps per side.  One workgroup per 32 x 64 output tile of a plane:
-// x is staged in LDS with a 2l halo (circular wrap on load), r = A x - y is formed in LDS
-// on the tile + l halo, then A^T r; the taps sit in LDS and are read as broadcasts.
+// depthwise, K = 2l+1 taps per side (the same for every channel).  One workgroup per 32 x 64
+// output tile of a plane: x is staged in LDS with a 2l halo (circular wrap on load), r = A x - y
+// is formed in LDS on the tile + l halo, then g = -(A^T r) / sigma2.  Register blocking: a
+// thread produces 4 adjacent columns from one (4 + 2l)-wide LDS row segment per tap row
+// (ds_read_b128), and the taps are kernel arguments (compile-time indices -> SGPR operands).
 // With Y != NULL the Langevin update Y = (X + c1 g) + c2 Z is fused (g is never stored).
 // ---------------------------------------------------------------------------------------
 constexpr int BL_TH = 32, BL_TW = 64, BL_MAXL = 8, BL_THREADS = 256;
-constexpr int BL_XH = BL_TH + 4 * BL_MAXL, BL_XW = BL_TW + 4 * BL_MAXL;
-constexpr int BL_RH = BL_TH + 2 * BL_MAXL, BL_RW = BL_TW + 2 * BL_MAXL;
+constexpr int BL_MAXK = 2 * BL_MAXL + 1;
 
 struct BlurArgs {
     const float* X;
     const float* y;
     long long y_cs;
-    const float* hconv;
-    const float* hcorr;
-    int l;
+    float hconv[BL_MAXK * BL_MAXK];
+    float hcorr[BL_MAXK * BL_MAXK];
     float* g;
     float* Y;
     int B, C, H, W;
@@ -1405,87 +1405,129 @@ struct BlurArgs {
     int chain0;
     const long long* d_step;
     long long off;
-    int exact;
     int tiles_x;
 };
 
-template <bool EXACT>
+template <bool EXACT, int L>
 __global__ void __launch_bounds__(BL_THREADS) blur_grad_kernel(const BlurArgs a) {
-    __shared__ float xs[BL_XH][BL_XW + 1];
-    __shared__ float rs[BL_RH][BL_RW + 1];
-    __shared__ float hc[(2 * BL_MAXL + 1) * (2 * BL_MAXL + 1)];
-    __shared__ float hr[(2 * BL_MAXL + 1) * (2 * BL_MAXL + 1)];
-    const int l = a.l, K = 2 * l + 1, H = a.H, W = a.W;
+    constexpr int K = 2 * L + 1;
+    constexpr int XH = BL_TH + 4 * L, XW = BL_TW + 4 * L;
+    constexpr int RH = BL_TH + 2 * L, RW = BL_TW + 2 * L;
+    constexpr int XS = ((XW + 3) & ~3) + 4, RS = ((RW + 3) & ~3) + 4;   // 16-B aligned row strides
+    constexpr int SEG = (4 + 2 * L + 3) / 4;                            // float4 reads per row segment
+    __shared__ __attribute__((aligned(16))) float xs[XH * XS];
+    __shared__ __attribute__((aligned(16))) float rs[RH * RS];
+    const int H = a.H, W = a.W;
     const int plane = blockIdx.y, b = plane / a.C, c = plane - b * a.C;
     const int ty = blockIdx.x / a.tiles_x, tx = blockIdx.x - ty * a.tiles_x;
     const int i0 = ty * BL_TH, j0 = tx * BL_TW;
     const size_t HW = (size_t)H * W;
     const float* xp = a.X + (size_t)plane * HW;
     const float* yp = a.y + (size_t)b * a.y_cs + (size_t)c * HW;
-    for (int t = threadIdx.x; t < K * K; t += BL_THREADS) { hc[t] = a.hconv[t]; hr[t] = a.hcorr[t]; }
-    // x on rows i0-2l .. i0+TH+2l-1, cols j0-2l .. j0+TW+2l-1 (circular)
-    const int xh = BL_TH + 4 * l, xw = BL_TW + 4 * l;
-    for (int t = threadIdx.x; t < xh * xw; t += BL_THREADS) {
-        const int p = t / xw, q = t - p * xw;
-        int gi = (i0 - 2 * l + p) % H; if (gi < 0) gi += H;
-        int gj = (j0 - 2 * l + q) % W; if (gj < 0) gj += W;
-        xs[p][q] = xp[(size_t)gi * W + gj];
+    // circular index; offsets are within 2l <= 16 of the plane, so this rarely loops (no division)
+    auto wrap = [](int v, int n) { while (v < 0) v += n; while (v >= n) v -= n; return v; };
+    // x on rows i0-2l .. i0+TH+2l-1, cols j0-2l .. j0+TW+2l-1 (circular padding applied twice)
+    for (int t = threadIdx.x; t < XH * XW; t += BL_THREADS) {
+        const int p = t / XW, q = t - p * XW;
+        xs[p * XS + q] = xp[(size_t)wrap(i0 - 2 * L + p, H) * W + wrap(j0 - 2 * L + q, W)];
     }
     __syncthreads();
-    // r = A x - y on rows i0-l .. i0+TH+l-1 (tap order a, b row-major)
-    const int rh = BL_TH + 2 * l, rw = BL_TW + 2 * l;
-    for (int t = threadIdx.x; t < rh * rw; t += BL_THREADS) {
-        const int p = t / rw, q = t - p * rw;
-        float acc = 0.0f;
-        for (int u = 0; u < K; ++u)
-            for (int v = 0; v < K; ++v) {
-                if (EXACT) acc = acc + hc[u * K + v] * xs[p + u][q + v];
-                else acc = __builtin_fmaf(hc[u * K + v], xs[p + u][q + v], acc);
+    // r = A x - y on rows i0-l .. i0+TH+l-1, cols j0-l .. j0+TW+l-1: strips of 4 columns
+    constexpr int RQ = (RW + 3) / 4;
+    for (int t = threadIdx.x; t < RH * RQ; t += BL_THREADS) {
+        const int p = t / RQ, q = (t - p * RQ) * 4;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            float row[SEG * 4];
+#pragma unroll
+            for (int sg = 0; sg < SEG; ++sg) {
+                const float4 v = *reinterpret_cast<const float4*>(&xs[(p + u) * XS + q + 4 * sg]);
+                row[4 * sg] = v.x; row[4 * sg + 1] = v.y; row[4 * sg + 2] = v.z; row[4 * sg + 3] = v.w;
             }
-        int gi = (i0 - l + p) % H; if (gi < 0) gi += H;
-        int gj = (j0 - l + q) % W; if (gj < 0) gj += W;
-        rs[p][q] = acc - yp[(size_t)gi * W + gj];
+#pragma unroll
+            for (int v = 0; v < K; ++v) {
+                const float hv = a.hconv[u * K + v];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    acc[k] = EXACT ? acc[k] + hv * row[k + v] : __builtin_fmaf(hv, row[k + v], acc[k]);
+            }
+        }
+        const int gi = wrap(i0 - L + p, H);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (q + k < RW) rs[p * RS + q + k] = acc[k] - yp[(size_t)gi * W + wrap(j0 - L + q + k, W)];
     }
     __syncthreads();
-    // g = -(A^T r) / sigma2 on the tile; a thread owns 4 consecutive columns x 2 rows
+    // g = -(A^T r) / sigma2 on the tile (+ the fused Langevin update)
     const long long step = (a.d_step ? *a.d_step : 0LL) + a.off;
-    const int tq = threadIdx.x & 15, tr = threadIdx.x >> 4;
-    for (int rr = 0; rr < 2; ++rr) {
-        const int p = tr * 2 + rr;
-        const int i = i0 + p;
-        if (i >= H) continue;
+    constexpr int TQ = BL_TW / 4;
+    for (int t = threadIdx.x; t < BL_TH * TQ; t += BL_THREADS) {
+        const int p = t / TQ, q = (t - p * TQ) * 4;
+        const int i = i0 + p, j = j0 + q;
+        if (i >= H || j >= W) continue;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            float row[SEG * 4];
+#pragma unroll
+            for (int sg = 0; sg < SEG; ++sg) {
+                const float4 v = *reinterpret_cast<const float4*>(&rs[(p + u) * RS + q + 4 * sg]);
+                row[4 * sg] = v.x; row[4 * sg + 1] = v.y; row[4 * sg + 2] = v.z; row[4 * sg + 3] = v.w;
+            }
+#pragma unroll
+            for (int v = 0; v < K; ++v) {
+                const float hv = a.hcorr[u * K + v];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    acc[k] = EXACT ? acc[k] + hv * row[k + v] : __builtin_fmaf(hv, row[k + v], acc[k]);
+            }
+        }
         float gv[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int q = tq * 4 + k;
-            float acc = 0.0f;
-            for (int u = 0; u < K; ++u)
-                for (int v = 0; v < K; ++v) {
-                    if (EXACT) acc = acc + hr[u * K + v] * rs[p + u][q + v];
-                    else acc = __builtin_fmaf(hr[u * K + v], rs[p + u][q + v], acc);
-                }
-            gv[k] = EXACT ? (-acc) / a.sigma2 : (-acc) * a.inv_sigma2;
-        }
-        const int j = j0 + tq * 4;
+        for (int k = 0; k < 4; ++k) gv[k] = EXACT ? (-acc[k]) / a.sigma2 : (-acc[k]) * a.inv_sigma2;
         const size_t e0 = (size_t)c * HW + (size_t)i * W + j;   // element index within the chain
         const size_t o = (size_t)b * a.C * HW + e0;
+        const bool full = (W & 3) == 0;                          // whole aligned quad in range
         if (a.Y) {
             float z[4];
-            if ((W & 3) == 0) {
+            if (full) {
                 normal_quad(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)(e0 >> 2), z);
             } else {
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                     z[k] = normal_elem(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint64_t)(e0 + k));
             }
+            if (full) {
+                const float4 xv = *reinterpret_cast<const float4*>(a.X + o);
+                const float xk[4] = {xv.x, xv.y, xv.z, xv.w};
+                float yv[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (j + k < W) a.Y[o + k] = (a.X[o + k] + a.c1 * gv[k]) + a.c2 * z[k];
+                for (int k = 0; k < 4; ++k) yv[k] = (xk[k] + a.c1 * gv[k]) + a.c2 * z[k];
+                *reinterpret_cast<float4*>(a.Y + o) = make_float4(yv[0], yv[1], yv[2], yv[3]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (j + k < W) a.Y[o + k] = (a.X[o + k] + a.c1 * gv[k]) + a.c2 * z[k];
+            }
+        } else if (full) {
+            *reinterpret_cast<float4*>(a.g + o) = make_float4(gv[0], gv[1], gv[2], gv[3]);
         } else {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (j + k < W) a.g[o + k] = gv[k];
         }
+    }
+}
+
+template <bool EXACT>
+static void launch_blur(const BlurArgs& a, int l, dim3 grid, hipStream_t st) {
+    switch (l) {
+#define PSGLA_BLUR_CASE(LL) case LL: hipLaunchKernelGGL((blur_grad_kernel<EXACT, LL>), grid, dim3(BL_THREADS), 0, st, a); break;
+        PSGLA_BLUR_CASE(0) PSGLA_BLUR_CASE(1) PSGLA_BLUR_CASE(2) PSGLA_BLUR_CASE(3) PSGLA_BLUR_CASE(4)
+        PSGLA_BLUR_CASE(5) PSGLA_BLUR_CASE(6) PSGLA_BLUR_CASE(7) PSGLA_BLUR_CASE(8)
+#undef PSGLA_BLUR_CASE
+        default: break;
     }
 }
 
@@ -1833,15 +1875,20 @@ int psgla_blur_grad(const float* X, const float* y, int64_t y_chain_stride, cons
     if (l < 0 || l > BL_MAXL) return fail(0, "psgla_blur_grad: blur half-width l outside [0, 8]");
     if ((long long)B * C > 65535) return fail(0, "psgla_blur_grad: more than 65535 planes in one launch");
     BlurArgs a;
-    a.X = X; a.y = y; a.y_cs = y_chain_stride; a.hconv = hconv; a.hcorr = hcorr; a.l = l; a.g = g; a.Y = Y;
+    memset(&a, 0, sizeof(a));
+    const int K = 2 * l + 1;
+    // the taps (HOST memory, like the scalars) travel as kernel arguments: SGPR operands
+    memcpy(a.hconv, hconv, sizeof(float) * K * K);
+    memcpy(a.hcorr, hcorr, sizeof(float) * K * K);
+    a.X = X; a.y = y; a.y_cs = y_chain_stride; a.g = g; a.Y = Y;
     a.B = B; a.C = C; a.H = H; a.W = W; a.sigma2 = sigma2; a.inv_sigma2 = (float)(1.0 / (double)sigma2);
     a.c1 = c1; a.c2 = c2; a.seed = seed; a.chain0 = chain0; a.d_step = (const long long*)d_step;
-    a.off = step_offset; a.exact = exact;
+    a.off = step_offset;
     a.tiles_x = (W + BL_TW - 1) / BL_TW;
     const int tiles_y = (H + BL_TH - 1) / BL_TH;
     const dim3 grid(a.tiles_x * tiles_y, B * C);
-    if (exact) hipLaunchKernelGGL(blur_grad_kernel<true>, grid, dim3(BL_THREADS), 0, (hipStream_t)stream, a);
-    else hipLaunchKernelGGL(blur_grad_kernel<false>, grid, dim3(BL_THREADS), 0, (hipStream_t)stream, a);
+    if (exact) launch_blur<true>(a, l, grid, (hipStream_t)stream);
+    else launch_blur<false>(a, l, grid, (hipStream_t)stream);
     return launch_check("blur_grad");
 }
 

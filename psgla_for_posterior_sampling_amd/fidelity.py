@@ -80,8 +80,8 @@ class BlurFidelity:
         hr = hcorr.reshape(-1, hcorr.shape[-2], hcorr.shape[-1])
         if not (torch.equal(hc, hc[:1].expand_as(hc)) and torch.equal(hr, hr[:1].expand_as(hr))):
             raise ValueError("BlurFidelity: per-channel blur kernels must be identical")
-        self.taps_conv = hc[0].contiguous().float()
-        self.taps_corr = hr[0].contiguous().float()
+        self.taps_conv = hc[0].float().cpu().numpy()        # host copies: launch arguments
+        self.taps_corr = hr[0].float().cpu().numpy()
 
     def A(self, x):
         l = self.l

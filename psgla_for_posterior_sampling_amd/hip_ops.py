@@ -152,15 +152,24 @@ def inpaint_grad(X, y, mask_u8, sigma2: float, out=None):
     return out
 
 
+def _host_taps(h, l: int) -> np.ndarray:
+    t = h.detach().cpu().numpy() if isinstance(h, torch.Tensor) else np.asarray(h)
+    t = np.ascontiguousarray(t, dtype=np.float32)
+    if t.shape != (2 * l + 1, 2 * l + 1):
+        raise ValueError(f"blur taps must be ({2 * l + 1}, {2 * l + 1}), got {t.shape}")
+    return t
+
+
 def blur_grad(X, y, hconv, hcorr, l: int, sigma2: float, out=None, exact: bool = False):
     """g = -A^T(A X - y) / sigma2 (circular depthwise (2l+1)^2 stencils, sampling_images.py:329-338).
-    hconv / hcorr: (2l+1, 2l+1) fp32 device taps shared by every channel."""
+    hconv / hcorr: (2l+1, 2l+1) fp32 taps shared by every channel (host copies are passed)."""
     B, C, H, W = X.shape
     if out is None:
         out = torch.empty_like(X)
     y_cs = 0 if y.shape[0] == 1 else C * H * W
-    N.check(N.lib().psgla_blur_grad(_ptr(X, name="X"), _ptr(y, name="y"), y_cs, _ptr(hconv, name="hconv"),
-                                    _ptr(hcorr, name="hcorr"), int(l), _ptr(out, name="g"), None, B, C, H, W,
+    hc, hr = _host_taps(hconv, l), _host_taps(hcorr, l)
+    N.check(N.lib().psgla_blur_grad(_ptr(X, name="X"), _ptr(y, name="y"), y_cs, hc.ctypes.data,
+                                    hr.ctypes.data, int(l), _ptr(out, name="g"), None, B, C, H, W,
                                     sigma2, 0.0, 0.0, 0, 0, None, 0, int(exact), _stream()), "psgla_blur_grad")
     return out
 
@@ -172,8 +181,9 @@ def blur_langevin(X, y, hconv, hcorr, l: int, sigma2: float, c1: float, c2: floa
     if out is None:
         out = torch.empty_like(X)
     y_cs = 0 if y.shape[0] == 1 else C * H * W
-    N.check(N.lib().psgla_blur_grad(_ptr(X, name="X"), _ptr(y, name="y"), y_cs, _ptr(hconv, name="hconv"),
-                                    _ptr(hcorr, name="hcorr"), int(l), None, _ptr(out, name="Y"), B, C, H, W,
+    hc, hr = _host_taps(hconv, l), _host_taps(hcorr, l)
+    N.check(N.lib().psgla_blur_grad(_ptr(X, name="X"), _ptr(y, name="y"), y_cs, hc.ctypes.data,
+                                    hr.ctypes.data, int(l), None, _ptr(out, name="Y"), B, C, H, W,
                                     sigma2, c1, c2, seed & (2 ** 64 - 1), chain0,
                                     d_step.data_ptr() if d_step is not None else None, step, int(exact),
                                     _stream()), "psgla_blur_grad")
