@@ -1361,18 +1361,23 @@ __global__ void normal_fill_kernel(float* out, int B, long long E, unsigned long
 __global__ void langevin_update_kernel(const float* X, const float* g, float* Y, int B, long long E,
                                        float c1, float c2, unsigned long long seed, int chain0,
                                        const long long* d_step, long long off) {
+    // grid: (quads of a chain, chain); one noise quad = 4 consecutive elements of the chain
     const long long step = read_step(d_step, off);
     const long long Q = (E + 3) >> 2;
-    const long long total = (long long)B * Q;
-    for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
-         t += (long long)gridDim.x * blockDim.x) {
-        const int b = (int)(t / Q);
-        const long long q = t - (long long)b * Q;
+    const int b = blockIdx.y;
+    const bool vec = (E & 3) == 0;
+    for (long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x; q < Q;
+         q += (long long)gridDim.x * blockDim.x) {
         float z[4];
         normal_quad(seed, (uint32_t)(chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)q, z);
         const size_t i0 = (size_t)b * E + (size_t)(q << 2);
-        for (int j = 0; j < 4; ++j) {
-            if ((q << 2) + j < E) Y[i0 + j] = (X[i0 + j] + c1 * g[i0 + j]) + c2 * z[j];
+        if (vec) {
+            const float4 x = ld4(X + i0), gg = ld4(g + i0);
+            st4(Y + i0, (x.x + c1 * gg.x) + c2 * z[0], (x.y + c1 * gg.y) + c2 * z[1],
+                (x.z + c1 * gg.z) + c2 * z[2], (x.w + c1 * gg.w) + c2 * z[3]);
+        } else {
+            for (int j = 0; j < 4; ++j)
+                if ((q << 2) + j < E) Y[i0 + j] = (X[i0 + j] + c1 * g[i0 + j]) + c2 * z[j];
         }
     }
 }
@@ -1574,11 +1579,75 @@ __device__ __forceinline__ void acc_elem(const AccArgs& s, long long step, size_
     }
 }
 
+// The schedule decisions of one step, hoisted out of the element loops.
+struct AccStep {
+    bool acc, first, blockend, sample;
+    long long blk, sidx;
+    float ca, cb;
+};
+__device__ __forceinline__ AccStep acc_step(const AccArgs& s, long long step, const float* mean) {
+    AccStep a;
+    a.acc = s.nm >= 0 && mean != nullptr;
+    const int per = s.nm + 1;
+    const int im = a.acc ? (int)(step % per) : 0;
+    a.first = im == 0;
+    a.blk = a.acc ? step / per : 0;
+    a.blockend = a.acc && im == s.nm;
+    a.ca = a.acc ? s.coef[2 * im] : 0.f;
+    a.cb = a.acc ? s.coef[2 * im + 1] : 0.f;
+    a.sample = s.n_inter > 0 && s.samples != nullptr && (step % s.n_inter) == 0;
+    a.sidx = a.sample ? step / s.n_inter : 0;
+    a.sample = a.sample && a.sidx < s.samples_cap;
+    return a;
+}
+// acc_elem's arithmetic on 4 aligned elements (idx % 4 == 0, 16-B accesses)
+__device__ __forceinline__ void acc_quad(const AccArgs& s, const AccStep& st, size_t idx, size_t BE, const float4& X,
+                                         float* mean, float* sq) {
+    if (st.acc) {
+        const float xs[4] = {X.x, X.y, X.z, X.w};
+        float m[4], q[4];
+        if (st.first) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { m[k] = st.cb * xs[k]; q[k] = st.cb * (xs[k] * xs[k]); }
+        } else {
+            const float4 mo = ld4(mean + idx), qo = ld4(sq + idx);
+            const float ms[4] = {mo.x, mo.y, mo.z, mo.w}, qs[4] = {qo.x, qo.y, qo.z, qo.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                m[k] = st.ca * ms[k] + st.cb * xs[k];
+                q[k] = st.ca * qs[k] + st.cb * (xs[k] * xs[k]);
+            }
+        }
+        if (st.blockend) {
+            if (st.blk < s.blocks_cap) {
+                st4(s.blocks + (size_t)st.blk * BE + idx, m[0], m[1], m[2], m[3]);
+                st4(s.blocks2 + (size_t)st.blk * BE + idx, q[0], q[1], q[2], q[3]);
+            }
+        } else {
+            st4(mean + idx, m[0], m[1], m[2], m[3]);
+            st4(sq + idx, q[0], q[1], q[2], q[3]);
+        }
+    }
+    if (st.sample) st4(s.samples + (size_t)st.sidx * BE + idx, X.x, X.y, X.z, X.w);
+}
+
 // X = (1 - alpha) Y + alpha D ; accumulate   (restoration_algorithms.py:238-271)
 __global__ void relax_accumulate_kernel(const float* Y, const float* D, float* X, float alpha,
                                         int B, long long E, float* mean, float* sq, AccArgs s) {
     const long long step = read_step(s.d_step, s.off);
     const size_t BE = (size_t)B * E;
+    if ((BE & 3) == 0) {
+        const AccStep st = acc_step(s, step, mean);
+        for (size_t i = 4 * (blockIdx.x * (size_t)blockDim.x + threadIdx.x); i < BE;
+             i += 4 * (size_t)gridDim.x * blockDim.x) {
+            const float4 y = ld4(Y + i), d = ld4(D + i);
+            const float4 x = make_float4((1.0f - alpha) * y.x + alpha * d.x, (1.0f - alpha) * y.y + alpha * d.y,
+                                         (1.0f - alpha) * y.z + alpha * d.z, (1.0f - alpha) * y.w + alpha * d.w);
+            st4(X + i, x.x, x.y, x.z, x.w);
+            acc_quad(s, st, i, BE, x, mean, sq);
+        }
+        return;
+    }
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < BE;
          i += (size_t)gridDim.x * blockDim.x) {
         const float x = (1.0f - alpha) * Y[i] + alpha * D[i];
@@ -1592,27 +1661,38 @@ __global__ void pnpula_update_kernel(const float* X, const float* gp, const floa
                                      float delta, float lambd, float brw, float cmin, float cmax, int B,
                                      long long E, float* mean, float* sq, unsigned long long seed,
                                      int chain0, AccArgs s) {
+    // grid: (quads of a chain, chain)
     const long long step = read_step(s.d_step, s.off);
     const long long Q = (E + 3) >> 2;
-    const long long total = (long long)B * Q;
     const size_t BE = (size_t)B * E;
-    for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
-         t += (long long)gridDim.x * blockDim.x) {
-        const int b = (int)(t / Q);
-        const long long q = t - (long long)b * Q;
+    const int b = blockIdx.y;
+    const bool vec = (E & 3) == 0;
+    const AccStep st = acc_step(s, step, mean);
+    for (long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x; q < Q;
+         q += (long long)gridDim.x * blockDim.x) {
         float z[4];
         normal_quad(seed, (uint32_t)(chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)q, z);
         const size_t i0 = (size_t)b * E + (size_t)(q << 2);
-        for (int j = 0; j < 4; ++j) {
-            if ((q << 2) + j >= E) break;
-            const size_t i = i0 + j;
-            const float x = X[i];
+        auto upd = [&](float x, float gpv, float gdv, float zz) {
             const float out = (x > cmin) ? x : cmin;
             const float proj = (out < cmax) ? out : cmax;
-            const float gpi = (gp[i] - (x - proj) / lambd) + gd[i];
-            const float xn = (x + delta * gpi) + brw * z[j];
-            Xo[i] = xn;
-            acc_elem(s, step, i, BE, xn, mean, sq);
+            const float gpi = (gpv - (x - proj) / lambd) + gdv;
+            return (x + delta * gpi) + brw * zz;
+        };
+        if (vec) {
+            const float4 x = ld4(X + i0), p4 = ld4(gp + i0), d4 = ld4(gd + i0);
+            const float4 xn = make_float4(upd(x.x, p4.x, d4.x, z[0]), upd(x.y, p4.y, d4.y, z[1]),
+                                          upd(x.z, p4.z, d4.z, z[2]), upd(x.w, p4.w, d4.w, z[3]));
+            st4(Xo + i0, xn.x, xn.y, xn.z, xn.w);
+            acc_quad(s, st, i0, BE, xn, mean, sq);
+        } else {
+            for (int j = 0; j < 4; ++j) {
+                if ((q << 2) + j >= E) break;
+                const size_t i = i0 + j;
+                const float xn = upd(X[i], gp[i], gd[i], z[j]);
+                Xo[i] = xn;
+                acc_elem(s, step, i, BE, xn, mean, sq);
+            }
         }
     }
 }
@@ -1620,13 +1700,28 @@ __global__ void pnpula_update_kernel(const float* X, const float* gp, const floa
 // g = ((-m) (X - y)) / sigma2   (sampling_images.py:295)
 __global__ void inpaint_grad_kernel(const float* X, const float* y, long long y_cs, const uint8_t* mask,
                                     long long m_cs, float* g, int B, int C, int H, int W, float sigma2) {
-    const size_t HW = (size_t)H * W, E = (size_t)C * HW, BE = (size_t)B * E;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < BE;
-         i += (size_t)gridDim.x * blockDim.x) {
-        const size_t b = i / E, e = i - b * E;
-        const size_t p = e % HW;
-        const float m = (float)mask[b * m_cs + p];
-        g[i] = (-m * (X[i] - y[b * y_cs + e])) / sigma2;
+    // grid: (quads of a plane, plane)
+    const size_t HW = (size_t)H * W;
+    const int plane = blockIdx.y, b = plane / C, c = plane - b * C;
+    const float* xp = X + (size_t)plane * HW;
+    const float* yp = y + (size_t)b * y_cs + (size_t)c * HW;
+    const uint8_t* mp = mask + (size_t)b * m_cs;
+    float* gq = g + (size_t)plane * HW;
+    if ((HW & 3) == 0) {
+        for (size_t i = 4 * (blockIdx.x * (size_t)blockDim.x + threadIdx.x); i < HW;
+             i += 4 * (size_t)gridDim.x * blockDim.x) {
+            const float4 x = ld4(xp + i), yy = ld4(yp + i);
+            const uint32_t m = *reinterpret_cast<const uint32_t*>(mp + i);
+            const float m0 = (float)(m & 0xFFu), m1 = (float)((m >> 8) & 0xFFu), m2 = (float)((m >> 16) & 0xFFu),
+                        m3 = (float)(m >> 24);
+            st4(gq + i, (-m0 * (x.x - yy.x)) / sigma2, (-m1 * (x.y - yy.y)) / sigma2,
+                (-m2 * (x.z - yy.z)) / sigma2, (-m3 * (x.w - yy.w)) / sigma2);
+        }
+        return;
+    }
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < HW; i += (size_t)gridDim.x * blockDim.x) {
+        const float m = (float)mp[i];
+        gq[i] = (-m * (xp[i] - yp[i])) / sigma2;
     }
 }
 
@@ -1665,6 +1760,15 @@ static int launch_check(const char* what) {
         return (int)e;
     }
     return 0;
+}
+
+// x-extent of a (work items of one chain / plane, chains) grid: ~4 waves of workgroups over the CUs
+static int grid_chain(long long per_chain, int chains) {
+    long long g = (per_chain + 255) / 256;
+    const long long cap = (4LL * 256 + chains - 1) / chains;   // total ~ 4 x 256 CUs x ... workgroups
+    if (g > cap * 4) g = cap * 4;
+    if (g < 1) g = 1;
+    return (int)g;
 }
 
 static int grid_for(long long n, int threads) {
@@ -1860,7 +1964,8 @@ int psgla_langevin_update(const float* X, const float* g, float* Y, int32_t B, i
                           void* stream) {
     if (!X || !g || !Y || B <= 0 || E <= 0) return fail(0, "psgla_langevin_update: bad arguments");
     const long long total = (long long)B * ((E + 3) / 4);
-    hipLaunchKernelGGL(langevin_update_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, X,
+    if (B > 65535) return fail(0, "psgla_langevin_update: more than 65535 chains in one launch");
+    hipLaunchKernelGGL(langevin_update_kernel, dim3(grid_chain(E / 4 + 1, B), B), dim3(256), 0, (hipStream_t)stream, X,
                        g, Y, B, (long long)E, c1, c2, (unsigned long long)seed, chain0,
                        (const long long*)d_step, (long long)step_offset);
     return launch_check("langevin_update");
@@ -1918,7 +2023,8 @@ int pnpula_update(const float* X, const float* gp, const float* gd, float* Xout,
     if (!X || !gp || !gd || !Xout || !s || B <= 0 || E <= 0) return fail(0, "pnpula_update: bad arguments");
     if (s->n_inter_mmse >= 0 && (!mean || !sq || !s->acc_coef)) return fail(0, "pnpula_update: accumulators missing");
     const long long total = (long long)B * ((E + 3) / 4);
-    hipLaunchKernelGGL(pnpula_update_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, X, gp,
+    if (B > 65535) return fail(0, "pnpula_update: more than 65535 chains in one launch");
+    hipLaunchKernelGGL(pnpula_update_kernel, dim3(grid_chain(E / 4 + 1, B), B), dim3(256), 0, (hipStream_t)stream, X, gp,
                        gd, Xout, delta, lambd, brw, c_min, c_max, B, (long long)E, mean, sq,
                        (unsigned long long)seed, chain0, make_acc(s));
     return launch_check("pnpula_update");
@@ -1929,7 +2035,9 @@ int psgla_inpaint_grad(const float* X, const float* y, int64_t y_chain_stride, c
                        void* stream) {
     if (!X || !y || !mask || !g || B <= 0 || C <= 0 || H <= 0 || W <= 0) return fail(0, "psgla_inpaint_grad: bad arguments");
     const long long total = (long long)B * C * H * W;
-    hipLaunchKernelGGL(inpaint_grad_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, X, y,
+    if ((long long)B * C > 65535) return fail(0, "psgla_inpaint_grad: more than 65535 planes in one launch");
+    hipLaunchKernelGGL(inpaint_grad_kernel, dim3(grid_chain((long long)H * W / 4 + 1, B * C), B * C), dim3(256), 0,
+                       (hipStream_t)stream, X, y,
                        (long long)y_chain_stride, mask, (long long)mask_chain_stride, g, B, C, H, W, sigma2);
     return launch_check("inpaint_grad");
 }
