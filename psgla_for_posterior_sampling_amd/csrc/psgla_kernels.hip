@@ -1136,6 +1136,23 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         // vector-memory stores per core row (all lanes of a wave store together; lane 0 is core)
         const int nst = 3 + (ALPHA1 ? 0 : 1) + ((si.acc && (si.blockend || si.liveout)) ? 2 : 0) + (si.sample ? 1 : 0);
         int pend = 0;   // stores issued after the DMA of the current row
+        // a row's stores are spread over the wave's two steps: state + accumulators, then the rest
+        bool hold = false;
+        size_t h_base = 0;
+        float4 hM = zero4, hQ = zero4, hX = zero4;
+        auto flush_held = [&]() {
+            if (!core) return;
+            if (si.acc) {
+                if (si.blockend) {
+                    st_sc1(a.blocks + (size_t)si.blk * BE + h_base, hM);
+                    st_sc1(a.blocks2 + (size_t)si.blk * BE + h_base, hQ);
+                } else if (si.liveout) {
+                    st_sc1(a.mean[par_out] + h_base, hM);
+                    st_sc1(a.sq[par_out] + h_base, hQ);
+                }
+            }
+            if (si.sample) st_sc1(a.samples + (size_t)si.sidx * BE + h_base, hX);
+        };
         back_issue(bw, rc_dma);
         for (int t = 0; t < nsteps; ++t) {
                 // ======================= BACK =======================
@@ -1196,20 +1213,17 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                         st_sc1(u2o, make_float4(U0.x, U1.x, U0.y, U1.y));
                         st_sc1(u2o + 4, make_float4(U0.z, U1.z, U0.w, U1.w));
                         if (!ALPHA1) st_sc1(a.x2[par_out] + base, X2);
-                        if (si.acc) {
-                            if (si.blockend) {
-                                st_sc1(a.blocks + (size_t)si.blk * BE + base, M4);
-                                st_sc1(a.blocks2 + (size_t)si.blk * BE + base, Q4);
-                            } else if (si.liveout) {
-                                st_sc1(a.mean[par_out] + base, M4);
-                                st_sc1(a.sq[par_out] + base, Q4);
-                            }
-                        }
-                        if (si.sample) st_sc1(a.samples + (size_t)si.sidx * BE + base, Xo);
+                        // the accumulator / sample stores go out in the wave's next (idle) step
+                        h_base = base; hM = M4; hQ = Q4; hX = Xo;
                     }
+                    hold = rowcore;
+                } else if (hold) {
+                    flush_held();
+                    hold = false;
                 }
             step_barrier(stp);
         }
+        if (hold) flush_held();
     }
 
 #ifdef PSGLA_STAMPS
