@@ -602,14 +602,15 @@ __device__ __forceinline__ void wait_vm_le(int n) {
     }
 }
 __device__ __forceinline__ void wait_vm_n(int n) { wait_vm_le<0>(n); }
-// 16-B store with sc1: the line leaves the XCD's L2 instead of staying dirty there, so the
-// end-of-pass agent release (buffer_wbl2) has almost nothing to write back.
+// 16-B streaming store (nt: the output rows are not re-read by this kernel).  Measured against
+// plain, sc1 and sc0 sc1 stores on the bench step: nt is the fastest (the per-workgroup agent
+// release before the arrival count still writes back whatever the XCD's L2 holds dirty).
 typedef float v4f __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void st_sc1(float* p, const float4& v) {
+__device__ __forceinline__ void st_nt(float* p, const float4& v) {
     const v4f x = {v.x, v.y, v.z, v.w};
     // s_nop: the compiler does not see this store, so it cannot pad the store-data hazard
     // (a VALU write of the data VGPRs right after a >8-byte store) -- the asm does
-    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
 }
 
 // Diagnostic build (-DPSGLA_STAMPS): every wave accumulates the cycles it spends working
@@ -1144,14 +1145,14 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
             if (!core) return;
             if (si.acc) {
                 if (si.blockend) {
-                    st_sc1(a.blocks + (size_t)si.blk * BE + h_base, hM);
-                    st_sc1(a.blocks2 + (size_t)si.blk * BE + h_base, hQ);
+                    st_nt(a.blocks + (size_t)si.blk * BE + h_base, hM);
+                    st_nt(a.blocks2 + (size_t)si.blk * BE + h_base, hQ);
                 } else if (si.liveout) {
-                    st_sc1(a.mean[par_out] + h_base, hM);
-                    st_sc1(a.sq[par_out] + h_base, hQ);
+                    st_nt(a.mean[par_out] + h_base, hM);
+                    st_nt(a.sq[par_out] + h_base, hQ);
                 }
             }
-            if (si.sample) st_sc1(a.samples + (size_t)si.sidx * BE + h_base, hX);
+            if (si.sample) st_nt(a.samples + (size_t)si.sidx * BE + h_base, hX);
         };
         back_issue(bw, rc_dma);
         for (int t = 0; t < nsteps; ++t) {
@@ -1208,11 +1209,11 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                     pend = rowcore ? nst : 0;
                     if (rowcore && core) {
                         const size_t base = plane_off(rc.p) + (size_t)rc.r * W + gj0;
-                        st_sc1(a.x[par_out] + base, Xo);
+                        st_nt(a.x[par_out] + base, Xo);
                         float* u2o = a.u2[par_out] + 2 * base;
-                        st_sc1(u2o, make_float4(U0.x, U1.x, U0.y, U1.y));
-                        st_sc1(u2o + 4, make_float4(U0.z, U1.z, U0.w, U1.w));
-                        if (!ALPHA1) st_sc1(a.x2[par_out] + base, X2);
+                        st_nt(u2o, make_float4(U0.x, U1.x, U0.y, U1.y));
+                        st_nt(u2o + 4, make_float4(U0.z, U1.z, U0.w, U1.w));
+                        if (!ALPHA1) st_nt(a.x2[par_out] + base, X2);
                         // the accumulator / sample stores go out in the wave's next (idle) step
                         h_base = base; hM = M4; hQ = Q4; hX = Xo;
                     }
@@ -1274,8 +1275,8 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
         }
     }
     // ---- step finalisation by the last workgroup to arrive (no second launch) ----
-    // Every wave's stores and atomics complete, then one agent release per workgroup (cheap: the
-    // outputs were stored sc1 and are not dirty in L2), then the arrival count.  The last
+    // Every wave's stores and atomics complete, then one agent release per workgroup (writes the
+    // XCD's dirty L2 lines back), then the arrival count.  The last
     // workgroup acquires before reading the rel-err sums or re-streaming a chain.
     wait_vm0();
     __syncthreads();
