@@ -1026,25 +1026,36 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         RowCursor rc_cur, rc_dma;
         cursor_init(rm, rc_cur, min(fw, Q - 1));
         cursor_init(rm, rc_dma, min(fw, Q - 1));
-        auto front_issue = [&](int q, const RowCursor& rc) {
+        // part `part` of the loads of stream row q: 0 = X, 1 = y, 2 = u2 (two halves), 3 = mask (+ x2)
+        auto front_issue = [&](int part, int q, const RowCursor& rc) {
             const int rr = min(rc.r, H - 1);
             const int bi = (q >> 2) & 1;
             const int bb = rc.p / C;
             const size_t base = plane_off(rc.p) + (size_t)rr * W + gjc;
-            glds16(xin + base, &sh.fst[fw][bi][0][0]);
-            glds16(a.yobs + (size_t)bb * a.y_cs + (size_t)(rc.p - bb * C) * HW + (size_t)rr * W + gjc,
-                   &sh.fst[fw][bi][1][0]);
-            glds16(u2in + 2 * base, &sh.fst[fw][bi][2][0]);
-            glds16(u2in + 2 * base + 4, &sh.fst[fw][bi][3][0]);
-            if (!ALPHA1) glds16(x2in + base, &sh.fst[fw][bi][4][0]);
-            glds4(a.mask + (size_t)bb * a.m_cs + (size_t)rr * W + gjc, &sh.fmk[fw][bi][0]);
+            if (part == 0) {
+                glds16(xin + base, &sh.fst[fw][bi][0][0]);
+            } else if (part == 1) {
+                glds16(a.yobs + (size_t)bb * a.y_cs + (size_t)(rc.p - bb * C) * HW + (size_t)rr * W + gjc,
+                       &sh.fst[fw][bi][1][0]);
+            } else if (part == 2) {
+                glds16(u2in + 2 * base, &sh.fst[fw][bi][2][0]);
+                glds16(u2in + 2 * base + 4, &sh.fst[fw][bi][3][0]);
+            } else {
+                if (!ALPHA1) glds16(x2in + base, &sh.fst[fw][bi][4][0]);
+                glds4(a.mask + (size_t)bb * a.m_cs + (size_t)rr * W + gjc, &sh.fmk[fw][bi][0]);
+            }
         };
-        front_issue(fw, rc_dma);
+        // row fw's loads up front; afterwards the loads of row q + 4 are issued one part per
+        // phase of row q (into the buffer of row q - 4, consumed before phase 0 of row q), so
+        // their issue cost is spread over four steps
+        for (int part = 0; part < 4; ++part) front_issue(part, fw, rc_dma);
+        cursor_advance(rm, rc_dma, min(4, max(0, Q - 1 - fw)));
         for (int t = 0; t < nsteps; ++t) {
                 // ======================= FRONT =======================
                 const int p = (t + 4 - fw) & 3;
                 const int q = t - p;
                 if (q >= 0 && q < Q) {
+                    if (p < 3) front_issue(p, q + 4, rc_dma);
                     if (p == 0) {
                         const int bb = rc_cur.p / C, cc = rc_cur.p - bb * C;
                         const size_t e = ((size_t)cc * H + rc_cur.r) * W + gj0;
@@ -1058,7 +1069,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                         box_muller(ph2, ph3, zn2, zn3);
                     } else {
                         STAMP_START(stp);
-                        wait_vm0();   // this wave's DMA of row q (issued 4 steps ago)
+                        wait_vm<ALPHA1 ? 4 : 4>();   // row q's loads landed; parts 0-2 of row q + 4 may fly
                         STAMP_SEG(stp, 0);
                         const int bi = (q >> 2) & 1;
                         const float4 fX = sh.fst[fw][bi][0][lane];
@@ -1096,9 +1107,9 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                         sh.y[q & (SP_YRING - 1)][lane] = Y4;
                         STAMP_SEG(stp, 2);
                         // the wave's next rows: noise row q + 4, DMA of row q + 8... issued as q + 4
+                        front_issue(3, q + 4, rc_dma);
                         cursor_advance(rm, rc_cur, 4);
-                        if (q + 4 < Q) cursor_advance(rm, rc_dma, 4);
-                        front_issue(q + 4, rc_dma);   // into the buffer of row q - 4 (consumed 4 steps ago)
+                        if (q + 8 < Q) cursor_advance(rm, rc_dma, 4);
                         STAMP_SEG(stp, 3);
                     }
                 }
