@@ -621,7 +621,7 @@ struct Stamps {
     int t = 0, w = 0;
     unsigned long long seg[4] = {0, 0, 0, 0}, ts = 0;
 };
-#ifdef PSGLA_STAMPS
+#ifdef PSGLA_STAMPS_SEG
 #define STAMP_SEG(st, i) do { const unsigned long long _n = stamp_now(); (st).seg[i] += _n - (st).ts; (st).ts = _n; } while (0)
 #define STAMP_START(st) do { (st).ts = stamp_now(); } while (0)
 #else
@@ -1147,7 +1147,6 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         };
         // vector-memory stores per core row (all lanes of a wave store together; lane 0 is core)
         const int nst = 3 + (ALPHA1 ? 0 : 1) + ((si.acc && (si.blockend || si.liveout)) ? 2 : 0) + (si.sample ? 1 : 0);
-        int pend = 0;   // stores issued after the DMA of the current row
         // a row's stores are spread over the wave's two steps: state + accumulators, then the rest
         bool hold = false;
         size_t h_base = 0;
@@ -1165,7 +1164,12 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
             }
             if (si.sample) st_nt(a.samples + (size_t)si.sidx * BE + h_base, hX);
         };
+        // mean / sq rows are LDS-DMA'd two of the wave's rows ahead (4 stream rows); c1 / c2 =
+        // vector-memory ops issued after the DMA of the wave's next / next-but-one row
         back_issue(bw, rc_dma);
+        if (bw + 2 < Q) cursor_advance(rm, rc_dma, 2);
+        back_issue(bw + 2, rc_dma);
+        int c1 = 2, c2 = 0;
         for (int t = 0; t < nsteps; ++t) {
                 // ======================= BACK =======================
                 const int q = t - 4 - 3 * n;
@@ -1187,7 +1191,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                         float4 bm = zero4, bq = zero4;
                         if (need_prev) {
                             // DMA of row q was issued just before the previous row's stores
-                            wait_vm_n(pend);
+                            wait_vm_n(c1);
                             bm = sh.bst[bw][(q >> 1) & 1][0][lane];
                             bq = sh.bst[bw][(q >> 1) & 1][1][lane];
                         }
@@ -1213,11 +1217,15 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                     const RowCursor rc = rc_cur;
                     cursor_advance(rm, rc_cur, 2);
-                    if (q + 2 < Q) cursor_advance(rm, rc_dma, 2);
-                    back_issue(q + 2, rc_dma);
+                    if (q + 4 < Q) cursor_advance(rm, rc_dma, 2);
+                    back_issue(q + 4, rc_dma);   // into the buffer just consumed (rows q, q + 4 share it)
                     asm volatile("" ::: "memory");
                     const bool rowcore = q >= qc0 && q < qc1;
-                    pend = rowcore ? nst : 0;
+                    {
+                        const int ns = rowcore ? nst : 0;   // this row's stores (both steps)
+                        c1 = c2 + 2 + ns;
+                        c2 = ns;
+                    }
                     if (rowcore && core) {
                         const size_t base = plane_off(rc.p) + (size_t)rc.r * W + gj0;
                         st_nt(a.x[par_out] + base, Xo);

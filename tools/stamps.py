@@ -27,7 +27,8 @@ init = mask_2d * y + (1 - mask_2d) * 0.5
 s = 10 / 255.0
 eng = FusedTvChains(init.contiguous().float(), y.contiguous().float(), mask_2d.to(torch.uint8), c1=1.5379e-4 * 10 / 10,
                     c2=0.0554594, sigma2=float(np.float32((1 / 255.0) ** 2)), alpha=1.0, ths=float(np.float32(s)),
-                    tv=K.TvConstants(n_it_max=NTV), seed=0, n_iter=10, n_inter=10, n_inter_mmse=10)
+                    tv=K.TvConstants(n_it_max=NTV), seed=0, n_iter=10, n_inter=10, n_inter_mmse=10,
+                    stream_wgs=-1)
 nsteps = H + 4 + 3 * NTV
 stamps = torch.zeros((B * C * 32 + nsteps * 32 + B * C * 16,), dtype=torch.int64, device=dev)
 eng.desc.debug_stamps = stamps.data_ptr()
