@@ -1121,6 +1121,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         // the left edge, the last row of u2[...,0] and the last column of u2[...,1] need no
         // select: the DPP shift feeds 0 at lane 0 and TV keeps those dual components exactly 0.
         const bool last3 = gj0 + CPL - 1 == W - 1;
+        __builtin_amdgcn_s_setprio(1);
         if (trk) stage_loop<EXACT, true>(a, sh, rm, k_st, nsteps, lane, last3, core, stp);
         else stage_loop<EXACT, false>(a, sh, rm, k_st, nsteps, lane, last3, core, stp);
     } else if (role == 3) {
@@ -1128,6 +1129,10 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
     } else {
         // ---------------- BACK state ----------------
         const int bw = w - SP_FRONT - n;                   // back wave id (stream rows q % 2 == bw)
+        // issue priority: back > stages > front.  The back waves are the youngest of the
+        // workgroup (lowest age priority) yet close every step (its last arrivals, measured);
+        // raising them, then the stages, cut the step by 9 % (A/B).
+        __builtin_amdgcn_s_setprio(3);
         const StepInfo si = step_info(a, step, a.mean[par_out]);
         const float* mean_in = a.mean[par_in];
         const float* sq_in = a.sq[par_in];
