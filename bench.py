@@ -51,6 +51,7 @@ def parse():
     p.add_argument("--kernel-iters", type=int, default=50)
     p.add_argument("--tv-iters", type=int, default=10, help="TV n_it_max (analysis only; the workload is 10)")
     p.add_argument("--stream-wgs", type=int, default=0, help="stream kernel work split (0 auto, -1 per plane)")
+    p.add_argument("--variant", choices=["auto", "band", "stream"], default="auto", help="fused TV kernel (analysis)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r01_pmc_tv_stream.json"))
@@ -147,7 +148,7 @@ def main():
                         sigma2=float(np.float32(sigma1 ** 2)), alpha=1.0, ths=float(np.float32(s)),
                         tv=K.TvConstants(n_it_max=args.tv_iters), seed=0, n_iter=n_iter + args.kernel_iters,
                         n_inter=n_inter, n_inter_mmse=nm, chain0=c0, exact=args.exact,
-                        stream_wgs=args.stream_wgs)
+                        stream_wgs=args.stream_wgs, kernel_variant=args.variant)
     gs = max(1, min(args.graph_steps, args.steps))
     # warm-up: eager steps + graph capture
     eng.step(max(1, args.warmup - gs))

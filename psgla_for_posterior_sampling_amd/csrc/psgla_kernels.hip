@@ -607,6 +607,9 @@ __device__ __forceinline__ void wait_vm_n(int n) { wait_vm_le<0>(n); }
 // release before the arrival count still writes back whatever the XCD's L2 holds dirty).
 typedef float v4f __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st_nt(float* p, const float4& v) {
+#ifdef PSGLA_ABL_NOSTORE
+    if (p) return;      // diagnostic timing build only: outputs are not written
+#endif
     const v4f x = {v.x, v.y, v.z, v.w};
     // s_nop: the compiler does not see this store, so it cannot pad the store-data hazard
     // (a VALU write of the data VGPRs right after a >8-byte store) -- the asm does
@@ -1028,6 +1031,9 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         cursor_init(rm, rc_dma, min(fw, Q - 1));
         // part `part` of the loads of stream row q: 0 = X, 1 = y, 2 = u2 (two halves), 3 = mask (+ x2)
         auto front_issue = [&](int part, int q, const RowCursor& rc) {
+#ifdef PSGLA_ABL_NOLOAD
+            return;     // diagnostic timing build only
+#endif
             const int rr = min(rc.r, H - 1);
             const int bi = (q >> 2) & 1;
             const int bb = rc.p / C;
@@ -1142,6 +1148,9 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         cursor_init(rm, rc_cur, min(bw, Q - 1));
         cursor_init(rm, rc_dma, min(bw, Q - 1));
         auto back_issue = [&](int q, const RowCursor& rc) {
+#ifdef PSGLA_ABL_NOLOAD
+            return;     // diagnostic timing build only
+#endif
             if (need_prev) {
                 const int rr = min(rc.r, H - 1);
                 const int bi = (q >> 1) & 1;
