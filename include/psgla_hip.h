@@ -150,6 +150,19 @@ int psgla_relax_accumulate(const float* Y, const float* D, float* X, float alpha
                            float* mean, float* sq, int32_t B, int64_t E, const PsglaSchedule* s,
                            void* stream);
 
+/* DNN-denoiser PSGLA, inpainting: the epilogue of step i fused with the prologue of step i+1
+ * (restoration_algorithms.py:238-271 then :232-236 with sampling_images.py:295):
+ *   X = (1-alpha)*Y + alpha*D  (X = D when alpha_is_one; Y may then be NULL);
+ *   samples / block accumulators of step i (PsglaSchedule, as psgla_relax_accumulate);
+ *   Y_next = (X + c1*g(X)) + c2*Z_{i+1},  g = ((-m)*(X - y))/sigma2,  Z_{i+1} the noise of step i+1;
+ *   X is stored only when X != NULL.  H*W % 4 == 0.  Identical to psgla_relax_accumulate +
+ *   psgla_inpaint_grad + psgla_langevin_update, in one pass (28 B/elem at alpha = 1). */
+int psgla_relax_langevin_inpaint(const float* Y, const float* D, float* X, float alpha, int32_t alpha_is_one,
+                                 const float* y, int64_t y_chain_stride, const uint8_t* mask,
+                                 int64_t mask_chain_stride, float* Y_next, float* mean, float* sq, int32_t B,
+                                 int32_t C, int32_t H, int32_t W, float sigma2, float c1, float c2, uint64_t seed,
+                                 int32_t chain0, const PsglaSchedule* s, void* stream);
+
 /* PnP-ULA update (restoration_algorithms.py:104-115) + samples / accumulators:
  *   proj = clip(X, c_min, c_max); X' = (X + delta*((gp - (X-proj)/lambd) + gd)) + brw*Z */
 int pnpula_update(const float* X, const float* gp, const float* gd, float* Xout, float delta,

@@ -68,6 +68,9 @@ _SIGNATURES = {
                                       c_i64, c_vp]),
     "psgla_relax_accumulate": (c_i32, [c_vp, c_vp, c_vp, c_f, c_i32, c_vp, c_vp, c_i32, c_i64,
                                        ctypes.POINTER(PsglaSchedule), c_vp]),
+    "psgla_relax_langevin_inpaint": (c_i32, [c_vp, c_vp, c_vp, c_f, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp,
+                                             c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_f, c_f, c_f, c_u64, c_i32,
+                                             ctypes.POINTER(PsglaSchedule), c_vp]),
     "pnpula_update": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_f, c_f, c_f, c_f, c_f, c_vp, c_vp, c_i32, c_i64,
                               c_u64, c_i32, ctypes.POINTER(PsglaSchedule), c_vp]),
     "psgla_inpaint_grad": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i32, c_i32, c_i32, c_i32, c_f,

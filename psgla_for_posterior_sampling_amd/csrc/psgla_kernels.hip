@@ -1704,6 +1704,52 @@ __global__ void relax_accumulate_kernel(const float* Y, const float* D, float* X
     }
 }
 
+// The DNN-denoiser PSGLA step's epilogue + the next step's prologue in one pass ("V-DnCNN"):
+//   X = (1 - alpha) Y + alpha D ; samples / accumulators of step i  (restoration_algorithms.py:238-271)
+//   Y' = (X + c1 g(X)) + c2 Z_{i+1},  g = ((-m)(X - y)) / sigma2    (:232-236, sampling_images.py:295)
+// X itself is written only when X_out != nullptr (the next relaxation needs Y' and D', not X).
+// Bit-identical to relax_accumulate + inpaint_grad + langevin_update (same operations, same order).
+// grid: (quads of a plane, plane)
+__global__ void relax_langevin_inpaint_kernel(const float* Y, const float* D, float* X_out, float alpha, int alpha1,
+                                              const float* y, long long y_cs, const uint8_t* mask, long long m_cs,
+                                              float* Y_next, int B, int C, int H, int W, float sigma2, float c1,
+                                              float c2, unsigned long long seed, int chain0, float* mean, float* sq,
+                                              AccArgs s) {
+    const long long step = read_step(s.d_step, s.off);
+    const size_t HW = (size_t)H * W;
+    const size_t E = (size_t)C * HW;
+    const size_t BE = (size_t)B * E;
+    const int plane = blockIdx.y, b = plane / C, c = plane - b * C;
+    const size_t p0 = (size_t)plane * HW;
+    const float* yp = y + (size_t)b * y_cs + (size_t)c * HW;
+    const uint8_t* mp = mask + (size_t)b * m_cs;
+    const AccStep st = acc_step(s, step, mean);
+    for (size_t i = 4 * (blockIdx.x * (size_t)blockDim.x + threadIdx.x); i < HW;
+         i += 4 * (size_t)gridDim.x * blockDim.x) {
+        const size_t idx = p0 + i;
+        const float4 d = ld4(D + idx);
+        float4 x = d;
+        if (!alpha1) {
+            const float4 yy = ld4(Y + idx);
+            x = make_float4((1.0f - alpha) * yy.x + alpha * d.x, (1.0f - alpha) * yy.y + alpha * d.y,
+                            (1.0f - alpha) * yy.z + alpha * d.z, (1.0f - alpha) * yy.w + alpha * d.w);
+        }
+        if (X_out) st4(X_out + idx, x.x, x.y, x.z, x.w);
+        acc_quad(s, st, idx, BE, x, mean, sq);
+        const float4 yo = ld4(yp + i);
+        const uint32_t m = *reinterpret_cast<const uint32_t*>(mp + i);
+        const float m0 = (float)(m & 0xFFu), m1 = (float)((m >> 8) & 0xFFu), m2 = (float)((m >> 16) & 0xFFu),
+                    m3 = (float)(m >> 24);
+        float z[4];
+        normal_quad(seed, (uint32_t)(chain0 + b), (uint32_t)(step + 1), TAG_LANGEVIN,
+                    (uint32_t)(((size_t)c * HW + i) >> 2), z);
+        const float g0 = (-m0 * (x.x - yo.x)) / sigma2, g1 = (-m1 * (x.y - yo.y)) / sigma2,
+                    g2 = (-m2 * (x.z - yo.z)) / sigma2, g3 = (-m3 * (x.w - yo.w)) / sigma2;
+        st4(Y_next + idx, (x.x + c1 * g0) + c2 * z[0], (x.y + c1 * g1) + c2 * z[1], (x.z + c1 * g2) + c2 * z[2],
+            (x.w + c1 * g3) + c2 * z[3]);
+    }
+}
+
 // PnP-ULA (restoration_algorithms.py:104-115)
 __global__ void pnpula_update_kernel(const float* X, const float* gp, const float* gd, float* Xo,
                                      float delta, float lambd, float brw, float cmin, float cmax, int B,
@@ -2088,6 +2134,25 @@ int psgla_inpaint_grad(const float* X, const float* y, int64_t y_chain_stride, c
                        (hipStream_t)stream, X, y,
                        (long long)y_chain_stride, mask, (long long)mask_chain_stride, g, B, C, H, W, sigma2);
     return launch_check("inpaint_grad");
+}
+
+int psgla_relax_langevin_inpaint(const float* Y, const float* D, float* X, float alpha, int32_t alpha_is_one,
+                                  const float* y, int64_t y_chain_stride, const uint8_t* mask,
+                                  int64_t mask_chain_stride, float* Y_next, float* mean, float* sq, int32_t B,
+                                  int32_t C, int32_t H, int32_t W, float sigma2, float c1, float c2, uint64_t seed,
+                                  int32_t chain0, const PsglaSchedule* s, void* stream) {
+    if (!D || !y || !mask || !Y_next || !s || B <= 0 || C <= 0 || H <= 0 || W <= 0)
+        return fail(0, "psgla_relax_langevin_inpaint: bad arguments");
+    if (!alpha_is_one && !Y) return fail(0, "psgla_relax_langevin_inpaint: Y required when alpha != 1");
+    if (((long long)H * W) % 4 != 0) return fail(0, "psgla_relax_langevin_inpaint: H*W must be a multiple of 4");
+    if (s->n_inter_mmse >= 0 && (!mean || !sq || !s->acc_coef))
+        return fail(0, "psgla_relax_langevin_inpaint: accumulators missing");
+    if ((long long)B * C > 65535) return fail(0, "psgla_relax_langevin_inpaint: more than 65535 planes in one launch");
+    hipLaunchKernelGGL(relax_langevin_inpaint_kernel, dim3(grid_chain((long long)H * W / 4 + 1, B * C), B * C),
+                       dim3(256), 0, (hipStream_t)stream, Y, D, X, alpha, (int)(alpha_is_one != 0), y,
+                       (long long)y_chain_stride, mask, (long long)mask_chain_stride, Y_next, B, C, H, W, sigma2, c1,
+                       c2, (unsigned long long)seed, chain0, mean, sq, make_acc(s));
+    return launch_check("relax_langevin_inpaint");
 }
 
 int psgla_debug_bm_tables(float* r, float* cs, float* sn, uint32_t k0, uint32_t n, void* stream) {

@@ -7,6 +7,14 @@
   layers, 64 features, ReLU, residual output; parameter names ``in_conv`` / ``conv_list.i`` /
   ``out_conv`` so a deepinv ``state_dict`` loads unchanged.  Runs on PyTorch-ROCm (MIOpen),
   as the north star prescribes for the DNN forward.
+* :class:`DRUNet` -- deepinv.models.DRUNet architecture (sampling_images.py:136; KAIR's UNetRes):
+  noise-level map as a 4th input channel, 4 scales (64/128/256/512 features), 4 residual blocks
+  per scale, 2x2 strided-conv down / transposed-conv up, no biases.  Restated from the published
+  deepinv 0.2.1 / KAIR layout (deepinv is not vendored in the reference and not installable
+  here): module names follow that layout so a ``drunet_color.pth`` state_dict would load, but
+  with neither the package nor the weights available its arithmetic is *parity unpinned*.
+* :class:`DenoiserPrior` -- the PnP-ULA prior gradient of sampling_images.py:156-157,
+  ``alpha * (D(x, s1) - x) / s2``, as a typed (capturable) callable.
 """
 from __future__ import annotations
 
@@ -80,10 +88,95 @@ class DnCNN(torch.nn.Module):
         return self.out_conv(x1) + x
 
 
+class _ResBlock(torch.nn.Module):
+    """x + conv3x3(relu(conv3x3(x))), no bias (KAIR ResBlock, mode 'CRC')."""
+
+    def __init__(self, nc: int):
+        super().__init__()
+        self.res = torch.nn.Sequential(torch.nn.Conv2d(nc, nc, 3, 1, 1, bias=False), torch.nn.ReLU(inplace=True),
+                                       torch.nn.Conv2d(nc, nc, 3, 1, 1, bias=False))
+
+    def forward(self, x):
+        return x + self.res(x)
+
+
+class DRUNet(torch.nn.Module):
+    """deepinv DRUNet(in_channels=3, out_channels=3, nc=[64, 128, 256, 512], nb=4, act_mode='R',
+    downsample_mode='strideconv', upsample_mode='convtranspose')."""
+
+    def __init__(self, in_channels: int = 3, out_channels: int = 3, nc=(64, 128, 256, 512), nb: int = 4,
+                 pretrained: str | None = None, device="cpu"):
+        super().__init__()
+        nn = torch.nn
+        self.m_head = nn.Conv2d(in_channels + 1, nc[0], 3, 1, 1, bias=False)
+        self.m_down1 = nn.Sequential(*[_ResBlock(nc[0]) for _ in range(nb)], nn.Conv2d(nc[0], nc[1], 2, 2, 0, bias=False))
+        self.m_down2 = nn.Sequential(*[_ResBlock(nc[1]) for _ in range(nb)], nn.Conv2d(nc[1], nc[2], 2, 2, 0, bias=False))
+        self.m_down3 = nn.Sequential(*[_ResBlock(nc[2]) for _ in range(nb)], nn.Conv2d(nc[2], nc[3], 2, 2, 0, bias=False))
+        self.m_body = nn.Sequential(*[_ResBlock(nc[3]) for _ in range(nb)])
+        self.m_up3 = nn.Sequential(nn.ConvTranspose2d(nc[3], nc[2], 2, 2, 0, bias=False), *[_ResBlock(nc[2]) for _ in range(nb)])
+        self.m_up2 = nn.Sequential(nn.ConvTranspose2d(nc[2], nc[1], 2, 2, 0, bias=False), *[_ResBlock(nc[1]) for _ in range(nb)])
+        self.m_up1 = nn.Sequential(nn.ConvTranspose2d(nc[1], nc[0], 2, 2, 0, bias=False), *[_ResBlock(nc[0]) for _ in range(nb)])
+        self.m_tail = nn.Conv2d(nc[0], out_channels, 3, 1, 1, bias=False)
+        if pretrained is not None and os.path.exists(pretrained):
+            sd = torch.load(pretrained, map_location="cpu", weights_only=True)
+            self.load_state_dict(sd, strict=True)
+        self.eval()
+        self.to(device)
+
+    def forward_unet(self, x0):
+        x1 = self.m_head(x0)
+        x2 = self.m_down1(x1)
+        x3 = self.m_down2(x2)
+        x4 = self.m_down3(x3)
+        x = self.m_body(x4)
+        x = self.m_up3(x + x4)
+        x = self.m_up2(x + x3)
+        x = self.m_up1(x + x2)
+        return self.m_tail(x + x1)
+
+    def forward(self, x, sigma):
+        if isinstance(sigma, torch.Tensor) and sigma.dim() > 0:
+            nmap = sigma.view(-1, 1, 1, 1).to(x.dtype) * torch.ones((x.size(0), 1, x.size(2), x.size(3)),
+                                                                      dtype=x.dtype, device=x.device)
+        else:
+            nmap = torch.full((x.size(0), 1, x.size(2), x.size(3)), float(sigma), dtype=x.dtype, device=x.device)
+        x = torch.cat((x, nmap), 1)
+        if x.size(2) % 8 == 0 and x.size(3) % 8 == 0:
+            return self.forward_unet(x)
+        # deepinv's test_pad: replicate-pad to a multiple of 8 (16 for images >= 32 px), crop back
+        h, w = x.size(2), x.size(3)
+        mod = 8 if (h < 32 or w < 32) else 16
+        ph, pw = (-h) % mod, (-w) % mod
+        y = self.forward_unet(torch.nn.functional.pad(x, (0, pw, 0, ph), mode="replicate"))
+        return y[..., :h, :w]
+
+
+def drunet_flops_per_pixel(nc=(64, 128, 256, 512), nb: int = 4, c: int = 3) -> float:
+    """2 x MACs per input pixel of the DRUNet forward (level k runs on 4^-k of the pixels)."""
+    macs = 9 * (c + 1) * nc[0] + 9 * nc[0] * c                        # head + tail
+    for k, n in enumerate(nc):
+        r = 4.0 ** -k
+        blocks = 2 * nb if k < len(nc) - 1 else nb                      # down + up resblocks (body: nb)
+        macs += r * blocks * 2 * 9 * n * n
+        if k + 1 < len(nc):
+            macs += (r / 4) * 4 * n * nc[k + 1] * 2                     # 2x2 down conv + 2x2 up transposed conv
+    return 2.0 * macs
+
+
+class DenoiserPrior:
+    """prior_grad(x) = alpha * (denoiser.forward(x, s1) - x) / s2   (sampling_images.py:156-157)."""
+
+    def __init__(self, denoiser, s1: float, alpha: torch.Tensor, s2: torch.Tensor):
+        self.denoiser, self.s1, self.alpha, self.s2 = denoiser, s1, alpha, s2
+
+    def __call__(self, x):
+        return self.alpha * (self.denoiser.forward(x, self.s1) - x) / self.s2
+
+
 def dncnn_flops_per_pixel(depth: int = 20, nf: int = 64, c: int = 3) -> float:
     """2 x MACs per output pixel of the DnCNN forward (1.334 MFLOP/pixel)."""
     macs = 9 * (c * nf + (depth - 2) * nf * nf + nf * c)
     return 2.0 * macs
 
 
-__all__ = ["TVDenoiser", "DnCNN", "dncnn_flops_per_pixel", "np"]
+__all__ = ["TVDenoiser", "DnCNN", "DRUNet", "DenoiserPrior", "dncnn_flops_per_pixel", "drunet_flops_per_pixel", "np"]

@@ -185,3 +185,166 @@ class FusedTvChains:
         if self.sched.blocks is None:
             return None, None
         return self.sched.blocks[:k], self.sched.blocks2[:k]
+
+
+def _capture(body, k: int, device):
+    """Record `k` calls of `body` into one hipGraph (torch.cuda.CUDAGraph) on a side stream."""
+    s = torch.cuda.Stream(device=device)
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        for _ in range(k):
+            body()
+    torch.cuda.current_stream().wait_stream(s)
+    return g
+
+
+class _GraphRunner:
+    """Eager / graph-replayed stepping shared by the DNN engines.  Buffer roles alternate by step
+    parity, so a graph holds an even number of steps and leaves them where it found them."""
+
+    steps_done: int
+    n_iter: int
+
+    def _body(self):  # pragma: no cover - abstract
+        raise NotImplementedError
+
+    def step(self, n: int = 1):
+        with torch.no_grad():
+            for _ in range(n):
+                if self.steps_done >= self.n_iter:
+                    raise RuntimeError("all n_iter steps already done")
+                self._body()
+                self.steps_done += 1
+
+    def capture(self, steps_per_graph: int):
+        k = steps_per_graph + (steps_per_graph & 1)
+        with torch.no_grad():
+            self.graph = _capture(self._body, k, self.device)
+        self.graph_steps = k
+
+    def replay(self, times: int = 1):
+        for _ in range(times):
+            if self.steps_done + self.graph_steps > self.n_iter:
+                raise RuntimeError("replay would exceed n_iter")
+            self.graph.replay()
+            self.steps_done += self.graph_steps
+
+    def run(self, n: int | None = None, graph_steps: int = 0):
+        n = self.n_iter - self.steps_done if n is None else n
+        # two eager steps first: the denoiser's kernels (MIOpen) pick their algorithms outside capture
+        warm = min(n, 2)
+        self.step(warm)
+        n -= warm
+        if graph_steps > 0 and n >= graph_steps:
+            if self.graph is None or self.graph_steps != graph_steps + (graph_steps & 1):
+                self.capture(graph_steps)
+            reps = n // self.graph_steps
+            self.replay(reps)
+            n -= reps * self.graph_steps
+        self.step(n)
+
+
+class DenoiserChains(_GraphRunner):
+    """B PSGLA chains with a PyTorch denoiser (DnCNN / DRUNet forward on PyTorch-ROCm) and a typed data
+    term: restoration_algorithms.py:231-271 with sampling_images.py:295 (inpainting) or :329-338
+    (deblurring).  Per step: ``D = denoiser.forward(Y, sigma)`` and then
+      inpainting: ONE HIP pass -- relaxation, accumulators / samples of step i and the next step's
+                  Langevin update Y' = (X + c1 g(X)) + c2 Z_{i+1}  (psgla_relax_langevin_inpaint);
+      deblurring: relaxation + accumulators, then the stencil kernel with the Langevin update fused.
+    The step index lives on the device, so steps [denoiser + HIP passes] are captured in one hipGraph
+    and replayed.  Identical results to the reference's loop order (the denoiser sees Y_i; X_{i+1}
+    is accumulated with step index i)."""
+
+    def __init__(self, init: torch.Tensor, data_grad, denoiser, sig_den, *, alpha: float, c1: float, c2: float,
+                 seed: int, n_iter: int, n_inter: int, n_inter_mmse: int, chain0: int = 0):
+        from .fidelity import BlurFidelity, InpaintingFidelity
+        if init.dim() != 4:
+            raise ValueError("init must be (B, C, H, W)")
+        self.inpaint = isinstance(data_grad, InpaintingFidelity)
+        if not (self.inpaint or isinstance(data_grad, BlurFidelity)):
+            raise TypeError("DenoiserChains needs an InpaintingFidelity or a BlurFidelity data term")
+        B, C, H, W = init.shape
+        if self.inpaint and (H * W) % 4:
+            raise ValueError("the fused inpainting pass needs H*W % 4 == 0")
+        self.device = init.device
+        self.shape = (B, C, H, W)
+        self.fid = data_grad
+        self.denoiser = denoiser
+        self.sig = sig_den
+        self.alpha = float(alpha)
+        self.c1, self.c2 = float(c1), float(c2)
+        self.seed, self.chain0 = int(seed), int(chain0)
+        self.n_iter = int(n_iter)
+        X0 = init.contiguous().float()
+        self.Y = [torch.empty_like(X0), torch.empty_like(X0)]
+        self.X = None if self.inpaint else torch.empty_like(X0)
+        self.mean = torch.zeros_like(X0)
+        self.sq = torch.zeros_like(X0)
+        self.sched = K.Schedule(self.shape, n_iter, n_inter, n_inter_mmse, self.device)
+        self.cur = 0
+        self.steps_done = 0
+        self.graph = None
+        self.graph_steps = 0
+        # prologue: Y_0 = (X_0 + c1 g(X_0)) + c2 Z_0
+        if self.inpaint:
+            g = K.inpaint_grad(X0, data_grad.y, data_grad.mask_u8, data_grad.sigma2)
+            K.langevin_update(X0, g, self.c1, self.c2, self.seed, self.chain0, 0, out=self.Y[0])
+        else:
+            f = data_grad
+            K.blur_langevin(X0, f.y.contiguous(), f.taps_conv, f.taps_corr, f.l, f.sigma2, self.c1, self.c2,
+                            self.seed, self.chain0, 0, out=self.Y[0], exact=f.exact)
+
+    def _body(self):
+        Yc, Yn = self.Y[self.cur], self.Y[1 - self.cur]
+        D = self.denoiser.forward(Yc, self.sig).contiguous().float()
+        f = self.fid
+        if self.inpaint:
+            K.relax_langevin_inpaint(Yc, D, self.alpha, f.y, f.mask_u8, f.sigma2, self.c1, self.c2, self.seed,
+                                     self.chain0, self.mean, self.sq, self.sched, 0, Yn, use_device_step=True)
+        else:
+            K.relax_accumulate(Yc, D, self.X, self.alpha, self.mean, self.sq, self.sched, 0, use_device_step=True)
+            K.blur_langevin(self.X, f.y.contiguous(), f.taps_conv, f.taps_corr, f.l, f.sigma2, self.c1, self.c2,
+                            self.seed, self.chain0, 1, out=Yn, exact=f.exact, d_step=self.sched.d_step)
+        K.advance_step(self.sched.d_step)
+        self.cur ^= 1
+
+
+class UlaChains(_GraphRunner):
+    """B PnP-ULA chains (restoration_algorithms.py:102-144) with a capturable prior gradient (e.g.
+    :class:`~psgla_for_posterior_sampling_amd.denoisers.DenoiserPrior` over DRUNet / DnCNN) and a
+    typed data term: per step the prior and data gradients, then one HIP pass (projection, update,
+    noise, accumulators); the step index lives on the device, so steps are hipGraph-replayed."""
+
+    def __init__(self, init: torch.Tensor, data_grad, prior_grad, *, delta: float, lambd: float, brw: float,
+                 c_min: float, c_max: float, seed: int, n_iter: int, n_inter: int, n_inter_mmse: int,
+                 chain0: int = 0):
+        self.device = init.device
+        X0 = init.contiguous().float().clone()
+        self.shape = tuple(X0.shape)
+        self.X = [X0, torch.empty_like(X0)]
+        self.mean = torch.zeros_like(X0)
+        self.sq = torch.zeros_like(X0)
+        self.data_grad, self.prior_grad = data_grad, prior_grad
+        self.delta, self.lambd, self.brw = float(delta), float(lambd), float(brw)
+        self.c_min, self.c_max = float(c_min), float(c_max)
+        self.seed, self.chain0 = int(seed), int(chain0)
+        self.n_iter = int(n_iter)
+        self.sched = K.Schedule(self.shape, n_iter, n_inter, n_inter_mmse, self.device)
+        self.cur = 0
+        self.steps_done = 0
+        self.graph = None
+        self.graph_steps = 0
+
+    def _body(self):
+        X, Xn = self.X[self.cur], self.X[1 - self.cur]
+        gp = self.prior_grad(X).contiguous().float()
+        gd = self.data_grad(X).contiguous().float()
+        K.pnpula_update(X, gp, gd, Xn, self.delta, self.lambd, self.brw, self.c_min, self.c_max, self.mean, self.sq,
+                        self.sched, 0, self.seed, self.chain0, use_device_step=True)
+        K.advance_step(self.sched.d_step)
+        self.cur ^= 1
+
+    @property
+    def state(self) -> torch.Tensor:
+        return self.X[self.cur]

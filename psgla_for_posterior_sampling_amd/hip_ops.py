@@ -128,6 +128,25 @@ def relax_accumulate(Y, D, X_out, alpha: float, mean, sq, sched: Schedule, step:
     return X_out
 
 
+def relax_langevin_inpaint(Y, D, alpha: float, y, mask_u8, sigma2: float, c1: float, c2: float, seed: int,
+                           chain0: int, mean, sq, sched: Schedule, step: int, Y_next, X_out=None,
+                           use_device_step: bool = False):
+    """Epilogue of step `step` + prologue of step `step + 1` for the inpainting fidelity (one pass):
+    X = (1-alpha) Y + alpha D, accumulators, Y_next = (X + c1 g(X)) + c2 Z_{step+1}."""
+    B, C, H, W = D.shape
+    alpha1 = float(alpha) == 1.0
+    y_cs = 0 if y.shape[0] == 1 else C * H * W
+    m_cs = 0 if (mask_u8.dim() == 2 or mask_u8.shape[0] == 1) else H * W
+    s = sched.struct(use_device_step, step)
+    N.check(N.lib().psgla_relax_langevin_inpaint(
+        None if alpha1 else _ptr(Y, name="Y"), _ptr(D, name="D"), _ptr(X_out, name="X") if X_out is not None else None,
+        float(alpha), int(alpha1), _ptr(y, name="y"), y_cs, _ptr(mask_u8, torch.uint8, "mask"), m_cs,
+        _ptr(Y_next, name="Y_next"), _ptr(mean, name="mean"), _ptr(sq, name="sq"), B, C, H, W, float(sigma2),
+        float(c1), float(c2), seed & (2 ** 64 - 1), int(chain0), ctypes.byref(s), _stream()),
+        "psgla_relax_langevin_inpaint")
+    return Y_next
+
+
 def pnpula_update(X, gp, gd, X_out, delta: float, lambd: float, brw: float, c_min: float, c_max: float,
                   mean, sq, sched: Schedule, step: int, seed: int, chain0: int, use_device_step: bool = False):
     B, E = _bce(X)

@@ -8,10 +8,17 @@ samples every ``n_inter`` steps, block means of X and of X**2) and error behavio
 Dispatch:
 * ``data_grad`` an :class:`InpaintingFidelity` and ``denoiser`` a :class:`TVDenoiser` ->
   the fused HIP step (one kernel launch per Langevin step, hipGraph-replayed): config 2.
-* anything else (opaque closures, torch denoisers) -> the closures are called as given,
-  and the rest of the step (Gaussian noise, Langevin update, relaxation, accumulators,
-  sample storage) runs as HIP kernels; a ``BlurFidelity`` data term is fused with the
-  Langevin update (one stencil kernel).
+* a typed data term (:class:`InpaintingFidelity` / :class:`BlurFidelity`) and a PyTorch
+  denoiser (DnCNN, DRUNet, any ``torch.nn.Module``) -> :class:`engine.DenoiserChains`: per step
+  the denoiser forward on PyTorch-ROCm, then one HIP pass (inpainting: relaxation, accumulators
+  and the next step's Langevin update fused) or two (deblurring: relaxation + accumulators, stencil
+  with the Langevin update fused); the step index lives on the device and, for this package's
+  DnCNN / DRUNet, ``graph_steps`` steps are captured in one hipGraph and replayed: configs 3-4.
+* anything else (opaque closures) -> the closures are called as given, and the rest of the
+  step (Gaussian noise, Langevin update, relaxation, accumulators, sample storage) runs as HIP
+  kernels; a ``BlurFidelity`` data term is fused with the Langevin update (one stencil kernel).
+``pnpula`` with a :class:`~denoisers.DenoiserPrior` prior and a typed data term runs
+:class:`engine.UlaChains` (hipGraph-replayed steps: config 5).
 The Gaussian noise is the in-kernel "psgla noise v1" stream of (seed, chain) instead of
 torch's generator (whose CUDA stream depends on the device's CU count); extra keyword
 ``chain0`` gives the global id of the first chain when a batch is sharded over GPUs.
@@ -27,8 +34,8 @@ import numpy as np
 import torch
 
 from . import hip_ops as K
-from .denoisers import TVDenoiser
-from .engine import FusedTvChains
+from .denoisers import DenoiserPrior, DnCNN, DRUNet, TVDenoiser
+from .engine import DenoiserChains, FusedTvChains, UlaChains
 from .fidelity import BlurFidelity, InpaintingFidelity
 
 DEFAULT_GRAPH_STEPS = int(os.environ.get("PSGLA_GRAPH_STEPS", "50"))
@@ -112,6 +119,17 @@ def psgla(init, data_grad, denoiser, alpha, lambd, sig_float=0.0055, delta=4e-5,
         denoiser.restart = False
         return _lists(eng.sched, eng.steps_done)
 
+    typed = isinstance(data_grad, (InpaintingFidelity, BlurFidelity))
+    if (typed and isinstance(denoiser, torch.nn.Module) and not isinstance(denoiser, TVDenoiser)
+            and not save_images_online and not (isinstance(data_grad, InpaintingFidelity)
+                                                and (shape[2] * shape[3]) % 4)):
+        sig_den = torch.tensor(sig_noised).to(dev).to(torch.float32)
+        eng = DenoiserChains(X0, data_grad, denoiser, sig_den, alpha=alpha_f, c1=c1, c2=c2, seed=seed,
+                             n_iter=n_iter, n_inter=n_inter, n_inter_mmse=n_inter_mmse, chain0=chain0)
+        capturable = isinstance(denoiser, (DnCNN, DRUNet)) or getattr(denoiser, "capturable", False)
+        eng.run(n_iter, graph_steps=graph_steps if (capturable and n_iter >= 2 * graph_steps) else 0)
+        return _lists(eng.sched, eng.steps_done)
+
     # ---- generic path: opaque closures, HIP noise / update / relaxation / accumulators ----
     sched = K.Schedule(shape, n_iter, n_inter, n_inter_mmse, dev)
     X = X0
@@ -139,7 +157,8 @@ def psgla(init, data_grad, denoiser, alpha, lambd, sig_float=0.0055, delta=4e-5,
 
 
 def pnpula(init, data_grad, prior_grad, delta, lambd, n_iter=5000, n_inter=1000, n_inter_mmse=1000, seed=None,
-           device=None, c_min=-1, c_max=2, path=None, save_images_online=False, name=None, *, chain0: int = 0):
+           device=None, c_min=-1, c_max=2, path=None, save_images_online=False, name=None, *, chain0: int = 0,
+           graph_steps: int | None = None):
     """PnP-ULA (restoration_algorithms.py:38-160)."""
     if not init.is_cuda:
         raise ValueError("pnpula runs on the GPU: init must be a CUDA (HIP) tensor")
@@ -152,12 +171,23 @@ def pnpula(init, data_grad, prior_grad, delta, lambd, n_iter=5000, n_inter=1000,
     dev = init.device
     X = init.clone().detach().contiguous().float()
     shape = X.shape
+    d = float(delta_t.cpu().item())
+    lam = float(torch.as_tensor(lambd).detach().cpu().to(torch.float32).item())
+    if graph_steps is None:
+        graph_steps = DEFAULT_GRAPH_STEPS
+    if (isinstance(prior_grad, DenoiserPrior) and isinstance(data_grad, (InpaintingFidelity, BlurFidelity))
+            and not save_images_online):
+        eng = UlaChains(X, data_grad, prior_grad, delta=d, lambd=lam, brw=brw, c_min=float(c_min),
+                        c_max=float(c_max), seed=int(seed), n_iter=n_iter, n_inter=n_inter,
+                        n_inter_mmse=n_inter_mmse, chain0=chain0)
+        capturable = isinstance(prior_grad.denoiser, (DnCNN, DRUNet)) or getattr(prior_grad.denoiser, "capturable",
+                                                                                False)
+        eng.run(n_iter, graph_steps=graph_steps if (capturable and n_iter >= 2 * graph_steps) else 0)
+        return _lists(eng.sched, eng.steps_done)
     sched = K.Schedule(shape, n_iter, n_inter, n_inter_mmse, dev)
     Xn = torch.empty_like(X)
     mean = torch.zeros_like(X)
     sq = torch.zeros_like(X)
-    d = float(delta_t.cpu().item())
-    lam = float(torch.as_tensor(lambd).detach().cpu().to(torch.float32).item())
     with torch.no_grad():
         for i in range(n_iter):
             gp = prior_grad(X).contiguous().float()

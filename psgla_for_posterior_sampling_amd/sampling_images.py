@@ -12,9 +12,9 @@ sample and of the running MMSE, std, ...) is metrics.analyse_run.
 
 Differences, all outside the hot path:
 * --alg pnp / red / diffpir / baseline are not part of this build (NotImplementedError);
-* --den DRUNet / GSDRUNet / Prox_DRUNet are not available (no deepinv, no weights); DnCNN loads
-  deepinv-format weights from --weights_dir (``--allow_random_weights`` runs a random-init
-  DnCNN for plumbing tests);
+* --den GSDRUNet / Prox_DRUNet are not available (no deepinv, no weights); DnCNN and DRUNet
+  (architectures restated in denoisers.py) load deepinv-format weights from --weights_dir
+  (``--allow_random_weights`` runs random-init networks for plumbing tests);
 * extra flags: --datasets_root, --weights_dir, --results_root, --no_plots,
   --allow_random_weights, --graph_steps.
 """
@@ -28,7 +28,7 @@ import numpy as np
 import torch
 
 from . import metrics
-from .denoisers import DnCNN, TVDenoiser
+from .denoisers import DenoiserPrior, DnCNN, DRUNet, TVDenoiser
 from .fidelity import deblurring_problem, inpainting_problem
 from .restoration_algorithms import pnpula, psgla
 
@@ -132,6 +132,11 @@ def make_denoiser(pars, device):
         if not os.path.exists(w) and not pars.allow_random_weights:
             raise FileNotFoundError(f"{w} not found (DnCNN weights; --allow_random_weights for plumbing runs)")
         return DnCNN(in_channels=3, out_channels=3, pretrained=w if os.path.exists(w) else None, device=device)
+    if pars.den == "DRUNet":
+        w = os.path.join(pars.weights_dir, "drunet_color.pth")
+        if not os.path.exists(w) and not pars.allow_random_weights:
+            raise FileNotFoundError(f"{w} not found (DRUNet weights; --allow_random_weights for plumbing runs)")
+        return DRUNet(in_channels=3, out_channels=3, pretrained=w if os.path.exists(w) else None, device=device)
     raise ValueError("Denoiser not implemented in this build: " + pars.den)
 
 
@@ -174,9 +179,9 @@ def restore_image(pars, argv, im: np.ndarray, denoiser, device, path_result_im: 
                                            lambd=lambdt, sig_float=s, delta=delta, **kw)
     else:
         s1, s2t = ex["s1"], torch.tensor(ex["s2"], dtype=dtype, device=device)
-
-        def prior_grad(x):
-            return alphat * (denoiser.forward(x, s1) - x) / s2t
+        prior_grad = DenoiserPrior(denoiser, s1, alphat, s2t)    # alphat*(D(x, s1) - x)/s2t (:156-157)
+        if pars.graph_steps is not None:
+            kw["graph_steps"] = pars.graph_steps
         Samples_t, Mmse_t, Mmse2_t = pnpula(init=init_torch, data_grad=data_grad, prior_grad=prior_grad,
                                             delta=torch.tensor(delta, dtype=dtype, device=device), lambd=lambdt,
                                             **kw)

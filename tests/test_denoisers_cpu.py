@@ -1,0 +1,43 @@
+"""CPU checks of the restated denoisers (no GPU needed): DRUNet layout / size / FLOPs, the
+DenoiserPrior arithmetic order (sampling_images.py:156-157)."""
+import torch
+
+from psgla_for_posterior_sampling_amd.denoisers import (DenoiserPrior, DnCNN, DRUNet, dncnn_flops_per_pixel,
+                                                        drunet_flops_per_pixel)
+
+
+def test_drunet_layout_and_size():
+    m = DRUNet()
+    assert sum(p.numel() for p in m.parameters()) == 32640960      # KAIR / deepinv drunet_color
+    keys = list(m.state_dict())
+    assert keys[0] == "m_head.weight" and keys[-1] == "m_tail.weight"
+    assert "m_down1.4.weight" in keys and "m_up3.0.weight" in keys and "m_body.3.res.2.weight" in keys
+    assert abs(drunet_flops_per_pixel() * 256 * 256 / 1e9 - 277.55) < 0.1
+
+
+def test_drunet_odd_sizes_and_sigma_map():
+    torch.manual_seed(0)
+    m = DRUNet(nc=(8, 16, 32, 64), nb=1)
+    with torch.no_grad():
+        for shape in [(1, 3, 24, 40), (2, 3, 33, 47), (1, 3, 16, 16)]:
+            x = torch.rand(shape)
+            assert m(x, 0.02).shape == x.shape
+        x = torch.rand(1, 3, 16, 24)
+        assert torch.equal(m(x, 0.02), m(x, torch.tensor([0.02])))
+
+
+def test_dncnn_size():
+    assert sum(p.numel() for p in DnCNN().parameters()) == 668227
+    assert abs(dncnn_flops_per_pixel() * 65536 / 1e9 - 87.43) < 0.01
+
+
+def test_denoiser_prior_matches_reference_closure():
+    torch.manual_seed(1)
+    den = DnCNN(depth=3, nf=8)
+    s1 = 5 / 255.0
+    alphat, s2t = torch.tensor(1.0), torch.tensor(s1 ** 2)
+    x = torch.rand(1, 3, 16, 16)
+    Ds = lambda x: den.forward(x, s1)                    # noqa: E731  (sampling_images.py:156-157)
+    ref = lambda x: alphat * (Ds(x) - x) / s2t           # noqa: E731
+    with torch.no_grad():
+        assert torch.equal(DenoiserPrior(den, s1, alphat, s2t)(x), ref(x))
