@@ -49,3 +49,27 @@ def test_cli_pnpula_deblurring_random_dncnn(tmp_path):
     recs = SI.main(argv)
     assert len(recs) == 1 and np.isfinite(recs[0]["PSNR_y"])
     assert len(recs[0]["PSNR_sample"]) == 1000    # n_inter = int(N / 1000) = 1: every step stored
+
+
+def test_cli_psgla_inpainting_random_dncnn(tmp_path):
+    """Config 3's command (--den DnCNN, random-init weights offline): the DenoiserChains path."""
+    from psgla_for_posterior_sampling_amd import sampling_images as SI
+    droot = _dataset(str(tmp_path), n=1)
+    argv = ["--alg", "psgla", "--den", "DnCNN", "--Pb", "inpainting", "--dataset_name", "synth", "--N", "1000",
+            "--datasets_root", droot, "--results_root", str(tmp_path / "results"), "--no_plots",
+            "--allow_random_weights", "--weights_dir", str(tmp_path / "none"), "--graph_steps", "20"]
+    recs = SI.main(argv)
+    assert len(recs) == 1 and np.isfinite(recs[0]["PSNR_MMSE"])
+    assert len(recs[0]["PSNR_sample"]) == 1000
+
+
+def test_cli_pnpula_inpainting_random_drunet(tmp_path):
+    """Config 5's command shape (--alg pnp_ula --den DRUNet): UlaChains with a DenoiserPrior."""
+    from psgla_for_posterior_sampling_amd import sampling_images as SI
+    droot = _dataset(str(tmp_path), n=1)
+    argv = ["--alg", "pnp_ula", "--den", "DRUNet", "--Pb", "inpainting", "--dataset_name", "synth", "--N", "1000",
+            "--s", "5", "--datasets_root", droot, "--results_root", str(tmp_path / "results"), "--no_plots",
+            "--allow_random_weights", "--weights_dir", str(tmp_path / "none"), "--graph_steps", "20"]
+    recs = SI.main(argv)
+    assert len(recs) == 1 and np.isfinite(recs[0]["PSNR_y"])
+    assert len(recs[0]["PSNR_sample"]) == 1000

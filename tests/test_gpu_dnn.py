@@ -141,3 +141,19 @@ def test_drunet_forward_on_gpu():
         yc = m.cpu()(x.cpu(), 5 / 255.0)
     assert y.shape == x.shape
     assert rel(y.cpu().numpy(), yc.numpy()) < 1e-4
+
+
+def test_denoiser_chains_independent_of_batch_split():
+    """Chains keyed by global id (chain0): a 4-chain run == two 2-chain runs (multi-GPU sharding)."""
+    from psgla_for_posterior_sampling_amd import restoration_algorithms as RA
+    dg, init = problem(B=4)
+    g = torch.Generator(device=DEV).manual_seed(8)
+    init = (init + 0.05 * torch.rand(init.shape, generator=g, device=DEV)).contiguous()
+    den = small_dncnn(seed=4).to(DEV)
+    kw = dict(sig_float=2 / 255.0, delta=6.1515e-5, n_iter=20, n_inter=5, n_inter_mmse=4, seed=3, graph_steps=4)
+    full = RA.psgla(init, dg, den, torch.tensor(1.0), torch.tensor(5.0), **kw)
+    lo = RA.psgla(init[:2].contiguous(), dg, den, torch.tensor(1.0), torch.tensor(5.0), chain0=0, **kw)
+    hi = RA.psgla(init[2:].contiguous(), dg, den, torch.tensor(1.0), torch.tensor(5.0), chain0=2, **kw)
+    for f, a, b in zip(full, lo, hi):
+        for u, v, w in zip(f, a, b):
+            assert torch.equal(u, torch.cat([v, w], 0))
