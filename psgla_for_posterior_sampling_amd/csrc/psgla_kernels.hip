@@ -1056,6 +1056,10 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         // their issue cost is spread over four steps
         for (int part = 0; part < 4; ++part) front_issue(part, fw, rc_dma);
         cursor_advance(rm, rc_dma, min(4, max(0, Q - 1 - fw)));
+#ifdef PSGLA_ABL_NOFRONT
+        for (int t = 0; t < nsteps; ++t) step_barrier(stp);   // diagnostic timing build only
+        if (nsteps >= 0) return;
+#endif
         for (int t = 0; t < nsteps; ++t) {
                 // ======================= FRONT =======================
                 const int p = (t + 4 - fw) & 3;
@@ -1133,6 +1137,10 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
     } else if (role == 3) {
         for (int t = 0; t < nsteps; ++t) step_barrier(stp);
     } else {
+#ifdef PSGLA_ABL_NOBACK
+        for (int t = 0; t < nsteps; ++t) step_barrier(stp);   // diagnostic timing build only
+        if (nsteps >= 0) return;
+#endif
         // ---------------- BACK state ----------------
         const int bw = w - SP_FRONT - n;                   // back wave id (stream rows q % 2 == bw)
         // issue priority: back > stages > front.  The back waves are the youngest of the
