@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PSGLA_HIP_ABI_VERSION 2
+#define PSGLA_HIP_ABI_VERSION 3
 
 /* Max inner TV iterations the fused (temporally blocked) kernel handles. */
 #define PSGLA_TV_MAX_FUSED_IT 24
@@ -108,6 +108,12 @@ typedef struct PsglaTvStep {
     int32_t stream_wgs;       /* streaming kernel work split: 0 auto (rows of all planes cut into
                                  one contiguous range per CU, n_tv halo rows at cuts, when W <= 256);
                                  -1 one workgroup per plane; > 0 force that many row ranges      */
+    int32_t ldw;              /* row pitch (elements) of every (.., H, W) buffer: x, u2 (x2 per
+                                 element pair), x2, mean, sq, y, mask, samples, blocks; 0 = W.
+                                 ldw != W (a multiple of 4 >= W: rows padded so that W % 4 != 0
+                                 images run on the streaming kernel) needs the streaming kernel;
+                                 the padding columns are scratch (never read into the image).
+                                 The noise stream is indexed by the unpadded element.            */
 } PsglaTvStep;
 
 int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream);

@@ -50,6 +50,7 @@ enum Front { FRONT_INPAINT = 0, FRONT_GIVEN = 1 };
 
 struct TvArgs {
     int B, C, H, W;
+    int ldw;                        // row pitch of every (.., H, W) buffer in elements (stream kernel; >= W)
     float* x[2];
     float* u2[2];
     float* x2[2];
@@ -786,10 +787,10 @@ struct StageRow {
     float x2n[CPL];           // x2^k of the row
 };
 
-template <bool EXACT, bool TRK>
+template <bool EXACT, bool TRK, bool GENW = false>
 __device__ __forceinline__ void stage_phase_a(const TvArgs& a, const float4& X2, const float4& U0,
                                               const float4& U1, const float4& YY, const float (&pu0)[CPL],
-                                              StageRow& o, float& sd, float& sn) {
+                                              StageRow& o, float& sd, float& sn, int nreal = CPL) {
     const float x2o[CPL] = {X2.x, X2.y, X2.z, X2.w};
     const float yy[CPL] = {YY.x, YY.y, YY.z, YY.w};
     o.u0[0] = U0.x; o.u0[1] = U0.y; o.u0[2] = U0.z; o.u0[3] = U0.w;
@@ -815,18 +816,21 @@ __device__ __forceinline__ void stage_phase_a(const TvArgs& a, const float4& X2,
             xn = __builtin_fmaf(a.rho, xv - xo, xo);
         }
         if (TRK) {
+            // padded rows (GENW): the lane's columns >= W are not part of the image's norms
+            const bool real = !GENW || kk < nreal;
             if (EXACT) {
-                const float d = xo - xn;
-                const float q = xn + 1e-12f;
+                const float d = real ? xo - xn : 0.f;
+                const float q = real ? xn + 1e-12f : 0.f;
                 sd = __builtin_fmaf(d, d, sd);
                 sn = __builtin_fmaf(q, q, sn);
             } else {
                 // ||x2_prev - x2|| = rho ||x - x2_prev||: accumulate (x - x2_prev)^2, scaled by rho^2
                 // when the sums are published; the +1e-12 of ||x2 + 1e-12|| is below fp32 resolution
                 // of any pixel value that contributes
-                const float d = xv - xo;
+                const float d = real ? xv - xo : 0.f;
+                const float q = real ? xn : 0.f;
                 sd = __builtin_fmaf(d, d, sd);
-                sn = __builtin_fmaf(xn, xn, sn);
+                sn = __builtin_fmaf(q, q, sn);
             }
         }
         o.z[kk] = zv;
@@ -834,9 +838,11 @@ __device__ __forceinline__ void stage_phase_a(const TvArgs& a, const float4& X2,
     }
 }
 
-template <bool EXACT, bool DN>
+// lastk: index (0..3) of the image's last column among this lane's columns, else outside 0..3
+// (GENW = false: the image's last column is always the last one of a lane)
+template <bool EXACT, bool DN, bool GENW = false>
 __device__ __forceinline__ void stage_phase_b(const TvArgs& a, const StageRow& ri, const float (&zj)[CPL],
-                                              bool last3, float (&un0)[CPL], float (&un1)[CPL]) {
+                                              int lastk, float (&un0)[CPL], float (&un1)[CPL]) {
     // z of the column right of this lane's last column (lane+1's first)
     const float zr3 = __int_as_float(
         __builtin_amdgcn_update_dpp(0, __float_as_int(ri.z[0]), 0x130 /* wave_shl:1 */, 0xF, 0xF, true));
@@ -847,7 +853,7 @@ __device__ __forceinline__ void stage_phase_b(const TvArgs& a, const StageRow& r
         // deepinv: (0 - z) + z_next == z_next - z exactly (up to the sign of a zero)
         const float g0 = DN ? (zj[kk] - zc) : 0.0f;
         float g1 = zr - zc;
-        if (kk == CPL - 1) g1 = last3 ? 0.0f : g1;
+        if (GENW || kk == CPL - 1) g1 = (lastk == kk) ? 0.0f : g1;
         const float uo0 = ri.u0[kk], uo1 = ri.u1[kk];
         if (EXACT) {
             const float v0 = uo0 + a.sig_tv * g0;
@@ -877,9 +883,9 @@ __device__ __forceinline__ void stage_phase_b(const TvArgs& a, const StageRow& r
 // Segment edges (split mode): the first row of a segment has no row above (its primal
 // uses u0 = 0 above) and the last has no row below (its dual has no vertical difference);
 // the rel-err partial sums are flushed per segment (different segments may be different chains).
-template <bool EXACT, bool TRK>
+template <bool EXACT, bool TRK, bool GENW>
 __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, const RowMap& rm, int k, int nsteps,
-                                           int lane, bool last3, bool core, Stamps& stp) {
+                                           int lane, int lastk, int nreal, bool core, Stamps& stp) {
     const int Q = rm.Q;
     const int tbeg = 1 + 3 * k;          // step of lookahead row 0
     StageRow RA, RB, RC;
@@ -901,7 +907,7 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
     auto primal = [&](int j, const float4& X2, const float4& U0, const float4& U1, const float4& YY,
                       const float (&pu0)[CPL], StageRow& cur) {
         float rd = 0.f, rn = 0.f;
-        stage_phase_a<EXACT, TRK>(a, X2, U0, U1, YY, pu0, cur, rd, rn);
+        stage_phase_a<EXACT, TRK, GENW>(a, X2, U0, U1, YY, pu0, cur, rd, rn, nreal);
         if (TRK && j >= qc0 && j < qc1) { lsd += rd; lsn += rn; }
     };
     int t = 0;
@@ -935,8 +941,8 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
         float4 X2, U0, U1, YY;
         load_row(j, X2, U0, U1, YY);
         float un0[CPL], un1[CPL];
-        if (!fprev) stage_phase_b<EXACT, true>(a, p2, p1.z, last3, un0, un1);
-        else stage_phase_b<EXACT, false>(a, p2, zero, last3, un0, un1);   // row j-2 ends a segment
+        if (!fprev) stage_phase_b<EXACT, true, GENW>(a, p2, p1.z, lastk, un0, un1);
+        else stage_phase_b<EXACT, false, GENW>(a, p2, zero, lastk, un0, un1);   // row j-2 ends a segment
         store_row(j - 2, p2, un0, un1);
         const bool fj = j == nb;
         if (fj) {                       // row j starts a new segment (split mode only)
@@ -961,10 +967,10 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
     // (static buffer roles per remainder: a runtime-indexed StageRow would go to scratch)
     auto finish = [&](StageRow& r2, StageRow& r1) {
         float un0[CPL], un1[CPL];
-        stage_phase_b<EXACT, true>(a, r2, r1.z, last3, un0, un1);
+        stage_phase_b<EXACT, true, GENW>(a, r2, r1.z, lastk, un0, un1);
         store_row(Q - 2, r2, un0, un1);
         step_barrier(stp);
-        stage_phase_b<EXACT, false>(a, r1, zero, last3, un0, un1);
+        stage_phase_b<EXACT, false, GENW>(a, r1, zero, lastk, un0, un1);
         store_row(Q - 1, r1, un0, un1);
         step_barrier(stp);
     };
@@ -987,14 +993,17 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
 // One pass of the row-streaming pipeline over the rows of `rm` with n inner TV iterations
 // (front / stage / back roles, one barrier per step).  Inlined at two call sites: the main
 // pass and the rare early-stop recompute, each with its own register allocation.
-template <bool EXACT, bool ALPHA1>
+// GENW: the row pitch is not the image width (rows padded: W % 4 != 0) -- the last-column, norm
+// and noise-window handling of such rows, compiled only into the kernels that need it
+template <bool EXACT, bool ALPHA1, bool GENW>
 __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, const RowMap& rm, const int n,
                                             const int cseg, const bool track, const long long step,
                                             const bool fresh, Stamps& stp) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (scalar branches)
     const int H = a.H, W = a.W, C = a.C;
-    const size_t HW = (size_t)H * W;
+    const int L = a.ldw;                                   // row pitch (memory); W: the image's width
+    const size_t HW = (size_t)H * L;                       // plane pitch
     const size_t E = (size_t)C * HW;
     const size_t BE = (size_t)a.B * E;
     const int par_in = (int)(step & 1), par_out = (int)((step + 1) & 1);
@@ -1020,12 +1029,15 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         const int fw = w;                                  // front wave id (stream rows q % 4 == fw)
         uint32_t ph0 = 0, ph1 = 0, ph2 = 0, ph3 = 0;
         float zn0 = 0.f, zn1 = 0.f, zn2 = 0.f, zn3 = 0.f;
+        uint32_t pq0 = 0, pq1 = 0, pq2 = 0, pq3 = 0;          // second quad (W % 4 != 0 rows)
+        float zq0 = 0.f, zq1 = 0.f, zq2 = 0.f, zq3 = 0.f;
+        int esh = 0;
         const float* xin = a.x[par_in];
         const float* u2in = a.u2[par_in];
         const float* x2in = ALPHA1 ? nullptr : a.x2[par_in];
         // The loads of a row are LDS-DMA'd 4 steps before the row is consumed (double-buffered
         // per front wave), row and column clamped into the plane so every lane loads.
-        const int gjc = min(gj0, W - CPL);
+        const int gjc = min(gj0, L - CPL);
         RowCursor rc_cur, rc_dma;
         cursor_init(rm, rc_cur, min(fw, Q - 1));
         cursor_init(rm, rc_dma, min(fw, Q - 1));
@@ -1037,18 +1049,18 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
             const int rr = min(rc.r, H - 1);
             const int bi = (q >> 2) & 1;
             const int bb = rc.p / C;
-            const size_t base = plane_off(rc.p) + (size_t)rr * W + gjc;
+            const size_t base = plane_off(rc.p) + (size_t)rr * L + gjc;
             if (part == 0) {
                 glds16(xin + base, &sh.fst[fw][bi][0][0]);
             } else if (part == 1) {
-                glds16(a.yobs + (size_t)bb * a.y_cs + (size_t)(rc.p - bb * C) * HW + (size_t)rr * W + gjc,
+                glds16(a.yobs + (size_t)bb * a.y_cs + (size_t)(rc.p - bb * C) * HW + (size_t)rr * L + gjc,
                        &sh.fst[fw][bi][1][0]);
             } else if (part == 2) {
                 glds16(u2in + 2 * base, &sh.fst[fw][bi][2][0]);
                 glds16(u2in + 2 * base + 4, &sh.fst[fw][bi][3][0]);
             } else {
                 if (!ALPHA1) glds16(x2in + base, &sh.fst[fw][bi][4][0]);
-                glds4(a.mask + (size_t)bb * a.m_cs + (size_t)rr * W + gjc, &sh.fmk[fw][bi][0]);
+                glds4(a.mask + (size_t)bb * a.m_cs + (size_t)rr * L + gjc, &sh.fmk[fw][bi][0]);
             }
         };
         // row fw's loads up front; afterwards the loads of row q + 4 are issued one part per
@@ -1068,15 +1080,35 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                     if (p < 3) front_issue(p, q + 4, rc_dma);
                     if (p == 0) {
                         const int bb = rc_cur.p / C, cc = rc_cur.p - bb * C;
+                        // element index in the chain's unpadded C*H*W image: the noise stream
+                        // does not depend on the row pitch
                         const size_t e = ((size_t)cc * H + rc_cur.r) * W + gj0;
+                        esh = (int)(e & 3);                         // the same for every lane of the row
                         uint32_t c0 = (uint32_t)(e >> 2), c1 = (uint32_t)step, c2 = TAG_LANGEVIN,
                                  c3 = (uint32_t)(a.seed >> 32);
                         philox4x32_10(c0, c1, c2, c3, (uint32_t)a.seed, (uint32_t)(a.chain0 + bb));
                         ph0 = c0; ph1 = c1; ph2 = c2; ph3 = c3;
+                        if (GENW && esh != 0) {                     // the lane's 4 elements span two quads
+                            uint32_t d0 = (uint32_t)(e >> 2) + 1u, d1 = (uint32_t)step, d2 = TAG_LANGEVIN,
+                                     d3 = (uint32_t)(a.seed >> 32);
+                            philox4x32_10(d0, d1, d2, d3, (uint32_t)a.seed, (uint32_t)(a.chain0 + bb));
+                            pq0 = d0; pq1 = d1; pq2 = d2; pq3 = d3;
+                        }
                     } else if (p == 1) {
                         box_muller(ph0, ph1, zn0, zn1);
+                        if (GENW && esh != 0) box_muller(pq0, pq1, zq0, zq1);
                     } else if (p == 2) {
                         box_muller(ph2, ph3, zn2, zn3);
+                        if (GENW && esh != 0) {
+                            box_muller(pq2, pq3, zq2, zq3);
+                            // element i of the lane = output (esh + i) of the two-quad window
+                            const float w8[8] = {zn0, zn1, zn2, zn3, zq0, zq1, zq2, zq3};
+                            float r4[CPL];
+#pragma unroll
+                            for (int i = 0; i < CPL; ++i)
+                                r4[i] = esh == 1 ? w8[i + 1] : (esh == 2 ? w8[i + 2] : w8[i + 3]);
+                            zn0 = r4[0]; zn1 = r4[1]; zn2 = r4[2]; zn3 = r4[3];
+                        }
                     } else {
                         STAMP_START(stp);
                         wait_vm<ALPHA1 ? 4 : 4>();   // row q's loads landed; parts 0-2 of row q + 4 may fly
@@ -1130,10 +1162,11 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         // the only column whose forward difference is forced to 0 is the image's right edge;
         // the left edge, the last row of u2[...,0] and the last column of u2[...,1] need no
         // select: the DPP shift feeds 0 at lane 0 and TV keeps those dual components exactly 0.
-        const bool last3 = gj0 + CPL - 1 == W - 1;
+        const int lastk = W - 1 - gj0;                    // in 0..3 on the lane holding column W-1
+        const int nreal = min(CPL, max(0, W - gj0));      // real (non-pitch-padding) columns of the lane
         __builtin_amdgcn_s_setprio(1);
-        if (trk) stage_loop<EXACT, true>(a, sh, rm, k_st, nsteps, lane, last3, core, stp);
-        else stage_loop<EXACT, false>(a, sh, rm, k_st, nsteps, lane, last3, core, stp);
+        if (trk) stage_loop<EXACT, true, GENW>(a, sh, rm, k_st, nsteps, lane, lastk, nreal, core, stp);
+        else stage_loop<EXACT, false, GENW>(a, sh, rm, k_st, nsteps, lane, lastk, nreal, core, stp);
     } else if (role == 3) {
         for (int t = 0; t < nsteps; ++t) step_barrier(stp);
     } else {
@@ -1151,7 +1184,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         const float* mean_in = a.mean[par_in];
         const float* sq_in = a.sq[par_in];
         const bool need_prev = si.acc && !si.first;
-        const int gjc = min(gj0, W - CPL);
+        const int gjc = min(gj0, L - CPL);
         RowCursor rc_cur, rc_dma;
         cursor_init(rm, rc_cur, min(bw, Q - 1));
         cursor_init(rm, rc_dma, min(bw, Q - 1));
@@ -1162,7 +1195,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
             if (need_prev) {
                 const int rr = min(rc.r, H - 1);
                 const int bi = (q >> 1) & 1;
-                const size_t base = plane_off(rc.p) + (size_t)rr * W + gjc;
+                const size_t base = plane_off(rc.p) + (size_t)rr * L + gjc;
                 glds16(mean_in + base, &sh.bst[bw][bi][0][0]);
                 glds16(sq_in + base, &sh.bst[bw][bi][1][0]);
             }
@@ -1249,7 +1282,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                         c2 = ns;
                     }
                     if (rowcore && core) {
-                        const size_t base = plane_off(rc.p) + (size_t)rc.r * W + gj0;
+                        const size_t base = plane_off(rc.p) + (size_t)rc.r * L + gj0;
                         st_nt(a.x[par_out] + base, Xo);
                         float* u2o = a.u2[par_out] + 2 * base;
                         st_nt(u2o, make_float4(U0.x, U1.x, U0.y, U1.y));
@@ -1282,7 +1315,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
     // early-stop test, per chain); the tracking stages wrote sh.red[segment][k - 1]
 }
 
-template <bool EXACT, bool ALPHA1>
+template <bool EXACT, bool ALPHA1, bool GENW>
 __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     __shared__ StreamShared sh;
     __shared__ int s_stop[MAXG];
@@ -1300,7 +1333,7 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
         RowMap rm;
         build_rowmap(a, blockIdx.x, rm);
         const int cseg = a.split_wgs > 0 ? 0 : blockIdx.x - (blockIdx.x / a.st_nsegs) * a.st_nsegs;
-        stream_pass<EXACT, ALPHA1>(a, sh, rm, a.n_tv, cseg, true, step, fresh, stp);
+        stream_pass<EXACT, ALPHA1, GENW>(a, sh, rm, a.n_tv, cseg, true, step, fresh, stp);
         if (!a.fin_inline) return;        // main-pass-only launch (kernel timing): no side effects
         // rel_err partial sums of this stream -> global, per segment's chain (deepinv's
         // early-stop test, per chain); the tracking stages wrote sh.red[segment][k - 1]
@@ -1373,7 +1406,7 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
         RowMap rm;
         plane_rowmap(a.H, plane, rm);
         const int nstop = __builtin_amdgcn_readfirstlane(s_stop[plane / C]);
-        stream_pass<EXACT, ALPHA1>(a, sh, rm, nstop, item - plane * a.st_nsegs, false, step, fresh, stp);
+        stream_pass<EXACT, ALPHA1, GENW>(a, sh, rm, nstop, item - plane * a.st_nsegs, false, step, fresh, stp);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < a.B * a.n_tv * 2; i += blockDim.x) a.norms[i] = 0.0;
@@ -1931,6 +1964,29 @@ static int choose_split(int B, int C, int H, int W, int h, int req, int* out) {
     return 0;
 }
 
+// Column segments of the streaming kernel: equal core widths (multiples of 4) cut from the image
+// width W; segment s's wave covers columns [f0, f0 + 256) with f0 = (cc0 - h) & ~3 (cc0 = s * seg_w),
+// which must reach cc1 + h for interior cuts (the TV dependency cone) and the row pitch L at the
+// image's right end (no halo needed at the image edges).  Fewest segments; 0 if none fits.
+static int stream_segments(int W, int L, int h, int* seg_w) {
+    for (int n = 1; n <= 64; ++n) {
+        const int sw = (((W + n - 1) / n) + 3) & ~3;
+        if ((long long)sw * (n - 1) >= W) continue;         // last segment would be empty
+        bool ok = true;
+        for (int sgi = 0; sgi < n && ok; ++sgi) {
+            const int cc0 = sgi * sw, cc1 = min(W, cc0 + sw);
+            const int f0 = max(0, cc0 - h) & ~3;
+            const int need = (cc1 >= W) ? L : min(L, cc1 + h);
+            ok = need - f0 <= TV_COLS;
+        }
+        if (ok) {
+            if (seg_w) *seg_w = sw;
+            return n;
+        }
+    }
+    return 0;
+}
+
 template <bool EXACT, int FRONT, bool ALPHA1>
 static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
     const int P = a.B * a.C;
@@ -1939,15 +1995,13 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
         if (FRONT == FRONT_INPAINT && a.stream) {
             TvArgs s = a;
             s.st_halo = a.n_tv;
-            if (a.W <= TV_COLS) { s.st_seg_w = a.W; s.st_nsegs = 1; }
-            else {
-                const int sw = (TV_COLS - 2 * s.st_halo - 3) & ~3;
-                s.st_nsegs = (a.W + sw - 1) / sw;
-                s.st_seg_w = (((a.W + s.st_nsegs - 1) / s.st_nsegs) + 3) & ~3;
-            }
+            s.st_nsegs = stream_segments(a.W, a.ldw, a.n_tv, &s.st_seg_w);
             s.fin_inline = (mask & 2) ? 1 : 0;
             const int grid = s.split_wgs > 0 ? s.split_wgs : P * s.st_nsegs;
-            hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+            if (s.ldw == s.W)
+                hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1, false>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+            else
+                hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1, true>), dim3(grid), dim3(TV_THREADS), 0, st, s);
             int rc = launch_check("tv_stream_kernel");
             if (rc) return rc;
             return 0;                    // finalised in-kernel (or main pass only)
@@ -1995,6 +2049,8 @@ int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream) {
     TvArgs a;
     memset(&a, 0, sizeof(a));
     a.B = d->B; a.C = d->C; a.H = d->H; a.W = d->W;
+    a.ldw = d->ldw > 0 ? d->ldw : d->W;
+    if (a.ldw < a.W) return fail(0, "psgla_tv_step: ldw < W");
     for (int i = 0; i < 2; ++i) {
         a.x[i] = d->x[i]; a.u2[i] = d->u2[i]; a.x2[i] = d->x2[i]; a.mean[i] = d->mean[i]; a.sq[i] = d->sq[i];
     }
@@ -2013,12 +2069,14 @@ int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream) {
     a.blocks = s->blocks; a.blocks2 = s->blocks2; a.blocks_cap = s->blocks_cap;
     a.halo = d->n_tv;
     tv_tiling(a);
-    const bool streamable = (d->W % 4 == 0) && d->n_tv >= 1 && d->n_tv <= SP_MAXST && d->H >= 2;
+    const bool streamable = (a.ldw % 4 == 0) && d->n_tv >= 1 && d->n_tv <= SP_MAXST && d->H >= 2 &&
+                            stream_segments(a.W, a.ldw, d->n_tv, nullptr) > 0;
     a.stream = streamable && d->kernel_variant != 1;
     if (d->kernel_variant == 2 && !streamable) return fail(0, "psgla_tv_step: shape not supported by the streaming kernel");
+    if (!a.stream && a.ldw != a.W) return fail(0, "psgla_tv_step: a row pitch ldw != W needs the streaming kernel");
     a.split_wgs = 0;
     if (a.stream) {
-        const int rc = choose_split(d->B, d->C, d->H, d->W, d->n_tv, d->stream_wgs, &a.split_wgs);
+        const int rc = choose_split(d->B, d->C, d->H, a.ldw, d->n_tv, d->stream_wgs, &a.split_wgs);
         if (rc) return rc;
     }
     hipStream_t st = (hipStream_t)stream;

@@ -33,24 +33,30 @@ class FusedTvChains:
         dev = init.device
         B, C, H, Wd = init.shape
         self.shape = (B, C, H, Wd)
+        self.W = Wd
+        # rows padded to a multiple of 4 columns so that every width runs on the streaming kernel
+        # (psgla_kernels.hip: ldw); the padding columns are scratch and every result is a view
+        # of the first W columns
+        self.ldw = Wd if (Wd % 4 == 0 or kernel_variant == "band") else (Wd + 3) // 4 * 4
+        self.pshape = (B, C, H, self.ldw)
         self.device = dev
         self.alpha = float(alpha)
         self.alpha1 = self.alpha == 1.0
         f32 = dict(dtype=torch.float32, device=dev)
-        self.x = [init.contiguous().clone(), torch.empty(self.shape, **f32)]
-        self.u2 = [torch.zeros(self.shape + (2,), **f32), torch.empty(self.shape + (2,), **f32)]
-        self.mean = [torch.zeros(self.shape, **f32), torch.zeros(self.shape, **f32)]
-        self.sq = [torch.zeros(self.shape, **f32), torch.zeros(self.shape, **f32)]
+        self.x = [self._padded(init), torch.zeros(self.pshape, **f32)]
+        self.u2 = [torch.zeros(self.pshape + (2,), **f32), torch.zeros(self.pshape + (2,), **f32)]
+        self.mean = [torch.zeros(self.pshape, **f32), torch.zeros(self.pshape, **f32)]
+        self.sq = [torch.zeros(self.pshape, **f32), torch.zeros(self.pshape, **f32)]
         self.x2 = None
         warm = tv_x2 is not None and tuple(tv_x2.shape) == self.shape
         if not self.alpha1 or warm:
-            self.x2 = [torch.empty(self.shape, **f32), torch.empty(self.shape, **f32)]
+            self.x2 = [torch.zeros(self.pshape, **f32), torch.zeros(self.pshape, **f32)]
         if warm:
-            self.x2[0].copy_(tv_x2)
-            self.u2[0].copy_(tv_u2)
-        self.y = y.contiguous()
-        self.mask = mask_u8.contiguous()
-        self.sched = K.Schedule(self.shape, n_iter, n_inter, n_inter_mmse, dev, store_samples, store_blocks)
+            self.x2[0][..., :Wd].copy_(tv_x2)
+            self.u2[0][..., :Wd, :].copy_(tv_u2)
+        self.y = self._padded(y)
+        self.mask = self._padded(mask_u8)
+        self.sched = K.Schedule(self.pshape, n_iter, n_inter, n_inter_mmse, dev, store_samples, store_blocks)
         self.work = K.TvWorkspace(B, tv.n_it, dev)
         self.work.fresh.fill_(0 if warm else 1)
         self.steps_done = 0
@@ -59,6 +65,7 @@ class FusedTvChains:
 
         d = N.PsglaTvStep()
         d.B, d.C, d.H, d.W = B, C, H, Wd
+        d.ldw = self.ldw
         for i in range(2):
             d.x[i] = self.x[i].data_ptr()
             d.u2[i] = self.u2[i].data_ptr()
@@ -66,9 +73,9 @@ class FusedTvChains:
             d.sq[i] = self.sq[i].data_ptr()
             d.x2[i] = self.x2[i].data_ptr() if (self.x2 is not None and not self.alpha1) else None
         d.y = K._ptr(self.y, name="y")
-        d.y_chain_stride = 0 if self.y.shape[0] == 1 else C * H * Wd
+        d.y_chain_stride = 0 if self.y.shape[0] == 1 else C * H * self.ldw
         d.mask = K._ptr(self.mask, torch.uint8, "mask")
-        d.mask_chain_stride = 0 if (self.mask.dim() == 2 or self.mask.shape[0] == 1) else H * Wd
+        d.mask_chain_stride = 0 if (self.mask.dim() == 2 or self.mask.shape[0] == 1) else H * self.ldw
         d.c1, d.c2, d.sigma2, d.alpha = c1, c2, sigma2, self.alpha
         d.tau, d.one_plus_tau, d.sigma_tv, d.rho = tv.tau, tv.one_plus_tau, tv.sigma_tv, tv.rho
         d.ths = float(np.float32(ths))
@@ -93,6 +100,20 @@ class FusedTvChains:
             self.desc_first = d0
         self.graph = None
         self.graph_steps = 0
+
+    def _padded(self, t: torch.Tensor) -> torch.Tensor:
+        """Contiguous copy of t (..., W) with rows padded by zeros to the row pitch ldw."""
+        t = t.contiguous()
+        if self.ldw == self.W:
+            return t.clone()
+        out = torch.zeros(t.shape[:-1] + (self.ldw,), dtype=t.dtype, device=t.device)
+        out[..., :self.W].copy_(t)
+        return out
+
+    def _view(self, t: torch.Tensor, u2: bool = False) -> torch.Tensor:
+        if t is None or self.ldw == self.W:
+            return t
+        return t[..., :self.W, :] if u2 else t[..., :self.W]
 
     # -- stepping -----------------------------------------------------------------
     def _launch(self, desc):
@@ -134,9 +155,10 @@ class FusedTvChains:
     @property
     def main_kernel(self) -> str:
         """Name of the kernel psgla_tv_step dispatches for this shape (psgla_kernels.hip:
-        streaming when W % 4 == 0, 1 <= n_tv <= 10 and H >= 2, unless the band kernel is forced)."""
+        streaming when the row pitch is a multiple of 4 -- always, the engine pads rows --,
+        1 <= n_tv <= 10 and H >= 2, unless the band kernel is forced)."""
         d = self.desc
-        streamable = d.W % 4 == 0 and 1 <= d.n_tv <= 10 and d.H >= 2
+        streamable = d.ldw % 4 == 0 and 1 <= d.n_tv <= 10 and d.H >= 2
         return "tv_stream_kernel" if streamable and d.kernel_variant != 1 else "tv_main_kernel"
 
     def launch_main_only(self, n: int = 1):
@@ -164,27 +186,39 @@ class FusedTvChains:
     # -- results --------------------------------------------------------------------
     @property
     def X(self) -> torch.Tensor:
-        return self.x[self.steps_done & 1]
+        return self._view(self.x[self.steps_done & 1])
 
     @property
     def u2_state(self) -> torch.Tensor:
-        return self.u2[self.steps_done & 1]
+        return self._view(self.u2[self.steps_done & 1], u2=True)
 
     @property
     def x2_state(self) -> torch.Tensor:
         if self.alpha1:
             return self.X
-        return self.x2[self.steps_done & 1]
+        return self._view(self.x2[self.steps_done & 1])
 
     def samples(self):
+        if self.sched.samples is None:
+            return None
         k = self.sched.n_samples_done(self.steps_done)
-        return self.sched.samples[:k] if k else self.sched.samples[:0] if self.sched.samples is not None else None
+        return self._view(self.sched.samples[:k])
 
     def blocks(self):
         k = self.sched.n_blocks_done(self.steps_done)
         if self.sched.blocks is None:
             return None, None
-        return self.sched.blocks[:k], self.sched.blocks2[:k]
+        return self._view(self.sched.blocks[:k]), self._view(self.sched.blocks2[:k])
+
+    def lists(self):
+        """The reference's return value: lists of squeezed (C, H, W) tensors (views of the stores)."""
+        ns = self.sched.n_samples_done(self.steps_done)
+        nb = self.sched.n_blocks_done(self.steps_done)
+        sm, (b1, b2) = self.samples(), self.blocks()
+        Xlist = [torch.squeeze(sm[k]) for k in range(ns)] if sm is not None else []
+        M = [torch.squeeze(b1[k]) for k in range(nb)] if b1 is not None else []
+        M2 = [torch.squeeze(b2[k]) for k in range(nb)] if b2 is not None else []
+        return Xlist, M, M2
 
 
 def _capture(body, k: int, device):

@@ -114,10 +114,10 @@ def psgla(init, data_grad, denoiser, alpha, lambd, sig_float=0.0055, delta=4e-5,
                             n_iter=n_iter, n_inter=n_inter, n_inter_mmse=n_inter_mmse, chain0=chain0,
                             exact=exact, tv_x2=denoiser.x2 if warm else None, tv_u2=denoiser.u2 if warm else None)
         eng.run(n_iter, graph_steps=graph_steps if n_iter >= 2 * graph_steps else 0)
-        denoiser.x2 = eng.x2_state.clone()
-        denoiser.u2 = eng.u2_state.clone()
+        denoiser.x2 = eng.x2_state.contiguous().clone()
+        denoiser.u2 = eng.u2_state.contiguous().clone()
         denoiser.restart = False
-        return _lists(eng.sched, eng.steps_done)
+        return eng.lists()
 
     typed = isinstance(data_grad, (InpaintingFidelity, BlurFidelity))
     if (typed and isinstance(denoiser, torch.nn.Module) and not isinstance(denoiser, TVDenoiser)

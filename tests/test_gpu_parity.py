@@ -477,3 +477,50 @@ def test_generic_psgla_deblur_matches_reference_fixture(bt):
     assert Xl.shape == fx["samples"].shape and Ml.shape == fx["blocks"].shape
     assert rel(Ml.mean(0), fx["blocks"].mean(0)) < REL_TOL_MEAN
     assert rel(M2l.mean(0), fx["blocks2"].mean(0)) < REL_TOL_MEAN
+
+
+@pytest.mark.parametrize("H,W,alpha", [(23, 29, 1.0), (19, 31, 1.0), (21, 33, 0.6), (16, 61, 1.0), (13, 301, 1.0),
+                                       (11, 483, 1.0)])
+def test_stream_padded_rows_exact_vs_oracle(H, W, alpha):
+    """W % 4 != 0 (rows padded to a multiple of 4 columns, the lane's 4 noise elements spanning two
+    quads at every offset) and W > 256 (column segments): the streaming kernel, bit-identical."""
+    B = 2
+    eng, (dg, y, init, mask2d, c1, c2) = _fused_batch(B, 5, exact=True, n_iter=12, H=H, W=W, alpha=alpha,
+                                                      variant="stream")
+    assert eng.main_kernel == "tv_stream_kernel"
+    eng.run(12, graph_steps=0)
+    torch.cuda.synchronize()
+    bm, bm2 = eng.blocks()
+    for b in range(B):
+        tv = orc.TVDenoiser(n_it_max=10)
+        Xl, Ml, M2l = orc.psgla(init, dg, tv, torch.tensor(alpha), torch.tensor(10.0), sig_float=10 / 255.0,
+                                delta=(10 / 255.0) ** 2, n_iter=12, n_inter=5, n_inter_mmse=4, seed=3, chain=5 + b)
+        np.testing.assert_array_equal(eng.samples()[:, b].cpu().numpy(), np.stack([t.numpy() for t in Xl]))
+        np.testing.assert_array_equal(bm[:, b].cpu().numpy(), np.stack([t.numpy() for t in Ml]))
+        np.testing.assert_array_equal(bm2[:, b].cpu().numpy(), np.stack([t.numpy() for t in M2l]))
+        np.testing.assert_array_equal(eng.u2_state[b].cpu().numpy(), tv.u2.numpy()[0])
+        np.testing.assert_array_equal(eng.x2_state[b].cpu().numpy(), tv.x2.numpy()[0])
+
+
+def test_psgla_padded_rows_returns_reference_shapes():
+    """The drop-in psgla() on an odd-width image: lists of (C, H, W) tensors, warm TV state (C, H, W)."""
+    from psgla_for_posterior_sampling_amd import restoration_algorithms as RA
+    from psgla_for_posterior_sampling_amd.denoisers import TVDenoiser
+    from psgla_for_posterior_sampling_amd.fidelity import InpaintingFidelity
+    g = torch.Generator().manual_seed(2)
+    x = torch.rand((1, 3, 21, 37), generator=g)
+    dg_ref, y, init, mask2d = orc.inpainting_problem(x, seed_ip=0)
+    dg = InpaintingFidelity(mask2d.to(DEV), y.to(DEV), torch.tensor((1 / 255.0) ** 2, dtype=torch.float32))
+    den = TVDenoiser(n_it_max=10, exact=True)
+    s = 10 / 255.0
+    out = RA.psgla(init.to(DEV), dg, den, torch.tensor(1.0), torch.tensor(10.0), sig_float=s, delta=s ** 2,
+                   n_iter=20, n_inter=10, n_inter_mmse=9, seed=0)
+    ref = orc.psgla(init, dg_ref, orc.TVDenoiser(n_it_max=10), torch.tensor(1.0), torch.tensor(10.0), sig_float=s,
+                    delta=s ** 2, n_iter=20, n_inter=10, n_inter_mmse=9, seed=0)
+    for a, b in zip(out, ref):
+        assert len(a) == len(b) > 0
+        for u, v in zip(a, b):
+            assert tuple(u.shape) == (3, 21, 37)
+            np.testing.assert_array_equal(u.cpu().numpy(), v.numpy())
+    assert tuple(den.x2.shape) == (1, 3, 21, 37) and den.x2.is_contiguous()
+    assert tuple(den.u2.shape) == (1, 3, 21, 37, 2)
