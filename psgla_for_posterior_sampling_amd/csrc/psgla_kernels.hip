@@ -710,10 +710,10 @@ __device__ __forceinline__ void build_rowmap(const TvArgs& a, int wg, RowMap& m)
     if (a.split_wgs <= 0) {
         m.ns = 1; m.Q = H; m.htop = 0; m.hbot = 0;
         m.q1 = m.q2 = m.q3 = H;
-        m.pl0 = wg / a.st_nsegs;
+        m.pl0 = wg;                   // virtual plane (plane * st_nsegs + column segment)
         return;
     }
-    const long long T = (long long)a.B * a.C * H;
+    const long long T = (long long)a.B * a.C * a.st_nsegs * H;
     const long long g0 = T * wg / a.split_wgs, g1 = T * (wg + 1) / a.split_wgs;
     const int p0 = (int)(g0 / H), p1 = (int)((g1 - 1) / H);
     const int h = a.n_tv;
@@ -751,6 +751,28 @@ __device__ __forceinline__ void plane_rowmap(int H, int plane, RowMap& m) {
     m.lo0 = m.lo1 = m.lo2 = m.lo3 = 0;
 }
 
+// Column geometry of a virtual plane vp = plane * st_nsegs + segment: the real plane, the start of the
+// segment's 256-column wave window (f0) and its core columns [cc0, cc1).  Without GEN there is one
+// segment (vp = plane, the whole row).
+struct SegGeo {
+    int rp, f0, cc0, cc1;
+};
+template <bool GEN>
+__device__ __forceinline__ SegGeo seg_geo(const TvArgs& a, int vp) {
+    SegGeo g;
+    if (!GEN) {
+        g.rp = vp; g.f0 = 0; g.cc0 = 0; g.cc1 = a.W;
+        return g;
+    }
+    const int ns = a.st_nsegs;
+    g.rp = vp / ns;
+    const int sgi = vp - g.rp * ns;
+    g.cc0 = sgi * a.st_seg_w;
+    g.cc1 = min(a.W, g.cc0 + a.st_seg_w);
+    g.f0 = max(0, g.cc0 - a.st_halo) & ~3;
+    return g;
+}
+
 // Position of a role's current row in the stream; advanced monotonically (the segment walk
 // runs only when a plane boundary is crossed).
 struct RowCursor {
@@ -785,9 +807,10 @@ struct StageRow {
     float u0[CPL], u1[CPL];   // u2^{k-1} of the row
     float z[CPL];             // z^k of the row
     float x2n[CPL];           // x2^k of the row
+    int lk;                   // GEN: the row's lastk (its column segment's), set by the primal
 };
 
-template <bool EXACT, bool TRK, bool GENW = false>
+template <bool EXACT, bool TRK, bool GEN = false>
 __device__ __forceinline__ void stage_phase_a(const TvArgs& a, const float4& X2, const float4& U0,
                                               const float4& U1, const float4& YY, const float (&pu0)[CPL],
                                               StageRow& o, float& sd, float& sn, int nreal = CPL) {
@@ -816,8 +839,8 @@ __device__ __forceinline__ void stage_phase_a(const TvArgs& a, const float4& X2,
             xn = __builtin_fmaf(a.rho, xv - xo, xo);
         }
         if (TRK) {
-            // padded rows (GENW): the lane's columns >= W are not part of the image's norms
-            const bool real = !GENW || kk < nreal;
+            // padded rows (GEN): the lane's columns >= W are not part of the image's norms
+            const bool real = !GEN || kk < nreal;
             if (EXACT) {
                 const float d = real ? xo - xn : 0.f;
                 const float q = real ? xn + 1e-12f : 0.f;
@@ -839,8 +862,8 @@ __device__ __forceinline__ void stage_phase_a(const TvArgs& a, const float4& X2,
 }
 
 // lastk: index (0..3) of the image's last column among this lane's columns, else outside 0..3
-// (GENW = false: the image's last column is always the last one of a lane)
-template <bool EXACT, bool DN, bool GENW = false>
+// (GEN = false: the image's last column is always the last one of a lane)
+template <bool EXACT, bool DN, bool GEN = false>
 __device__ __forceinline__ void stage_phase_b(const TvArgs& a, const StageRow& ri, const float (&zj)[CPL],
                                               int lastk, float (&un0)[CPL], float (&un1)[CPL]) {
     // z of the column right of this lane's last column (lane+1's first)
@@ -853,7 +876,7 @@ __device__ __forceinline__ void stage_phase_b(const TvArgs& a, const StageRow& r
         // deepinv: (0 - z) + z_next == z_next - z exactly (up to the sign of a zero)
         const float g0 = DN ? (zj[kk] - zc) : 0.0f;
         float g1 = zr - zc;
-        if (GENW || kk == CPL - 1) g1 = (lastk == kk) ? 0.0f : g1;
+        if (GEN || kk == CPL - 1) g1 = (lastk == kk) ? 0.0f : g1;
         const float uo0 = ri.u0[kk], uo1 = ri.u1[kk];
         if (EXACT) {
             const float v0 = uo0 + a.sig_tv * g0;
@@ -883,9 +906,21 @@ __device__ __forceinline__ void stage_phase_b(const TvArgs& a, const StageRow& r
 // Segment edges (split mode): the first row of a segment has no row above (its primal
 // uses u0 = 0 above) and the last has no row below (its dual has no vertical difference);
 // the rel-err partial sums are flushed per segment (different segments may be different chains).
-template <bool EXACT, bool TRK, bool GENW>
+template <bool EXACT, bool TRK, bool GEN>
 __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, const RowMap& rm, int k, int nsteps,
                                            int lane, int lastk, int nreal, bool core, Stamps& stp) {
+    // GEN: the lane's columns change with the column segment of the row (row split over virtual
+    // planes): lastk / nreal / core follow the primal row's segment; each row carries its lastk
+    // to its dual (StageRow.lk)
+    auto set_geo = [&](int sgi) {
+        if (GEN) {
+            const SegGeo g = seg_geo<GEN>(a, rm.pl(sgi));
+            const int gj = g.f0 + CPL * lane;
+            lastk = a.W - 1 - gj;
+            nreal = min(CPL, max(0, a.W - gj));
+            core = gj < a.W && gj >= g.cc0 && gj < g.cc1;
+        }
+    };
     const int Q = rm.Q;
     const int tbeg = 1 + 3 * k;          // step of lookahead row 0
     StageRow RA, RB, RC;
@@ -907,7 +942,8 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
     auto primal = [&](int j, const float4& X2, const float4& U0, const float4& U1, const float4& YY,
                       const float (&pu0)[CPL], StageRow& cur) {
         float rd = 0.f, rn = 0.f;
-        stage_phase_a<EXACT, TRK, GENW>(a, X2, U0, U1, YY, pu0, cur, rd, rn, nreal);
+        stage_phase_a<EXACT, TRK, GEN>(a, X2, U0, U1, YY, pu0, cur, rd, rn, nreal);
+        if (GEN) cur.lk = lastk;
         if (TRK && j >= qc0 && j < qc1) { lsd += rd; lsn += rn; }
     };
     int t = 0;
@@ -941,14 +977,15 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
         float4 X2, U0, U1, YY;
         load_row(j, X2, U0, U1, YY);
         float un0[CPL], un1[CPL];
-        if (!fprev) stage_phase_b<EXACT, true, GENW>(a, p2, p1.z, lastk, un0, un1);
-        else stage_phase_b<EXACT, false, GENW>(a, p2, zero, lastk, un0, un1);   // row j-2 ends a segment
+        if (!fprev) stage_phase_b<EXACT, true, GEN>(a, p2, p1.z, GEN ? p2.lk : lastk, un0, un1);
+        else stage_phase_b<EXACT, false, GEN>(a, p2, zero, GEN ? p2.lk : lastk, un0, un1);   // row j-2 ends a segment
         store_row(j - 2, p2, un0, un1);
         const bool fj = j == nb;
         if (fj) {                       // row j starts a new segment (split mode only)
             flush();
             ++sacc;
             nb = next_seg_start(rm, j);
+            set_geo(sacc);
             primal(j, X2, U0, U1, YY, zero, cur);
         } else {
             primal(j, X2, U0, U1, YY, p1.u0, cur);
@@ -967,10 +1004,10 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
     // (static buffer roles per remainder: a runtime-indexed StageRow would go to scratch)
     auto finish = [&](StageRow& r2, StageRow& r1) {
         float un0[CPL], un1[CPL];
-        stage_phase_b<EXACT, true, GENW>(a, r2, r1.z, lastk, un0, un1);
+        stage_phase_b<EXACT, true, GEN>(a, r2, r1.z, GEN ? r2.lk : lastk, un0, un1);
         store_row(Q - 2, r2, un0, un1);
         step_barrier(stp);
-        stage_phase_b<EXACT, false, GENW>(a, r1, zero, lastk, un0, un1);
+        stage_phase_b<EXACT, false, GEN>(a, r1, zero, GEN ? r1.lk : lastk, un0, un1);
         store_row(Q - 1, r1, un0, un1);
         step_barrier(stp);
     };
@@ -993,12 +1030,11 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
 // One pass of the row-streaming pipeline over the rows of `rm` with n inner TV iterations
 // (front / stage / back roles, one barrier per step).  Inlined at two call sites: the main
 // pass and the rare early-stop recompute, each with its own register allocation.
-// GENW: the row pitch is not the image width (rows padded: W % 4 != 0) -- the last-column, norm
+// GEN: the row pitch is not the image width (rows padded: W % 4 != 0) -- the last-column, norm
 // and noise-window handling of such rows, compiled only into the kernels that need it
-template <bool EXACT, bool ALPHA1, bool GENW>
+template <bool EXACT, bool ALPHA1, bool GEN>
 __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, const RowMap& rm, const int n,
-                                            const int cseg, const bool track, const long long step,
-                                            const bool fresh, Stamps& stp) {
+                                            const bool track, const long long step, const bool fresh, Stamps& stp) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (scalar branches)
     const int H = a.H, W = a.W, C = a.C;
@@ -1011,11 +1047,12 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
     auto plane_off = [&](int pl) -> size_t { return (size_t)pl * HW; };   // planes are (b, c) in NCHW order
     const int Q = rm.Q;
     const int qc0 = rm.htop, qc1 = Q - rm.hbot;          // core stream rows
-    const int cc0 = cseg * a.st_seg_w, cc1 = min(W, cc0 + a.st_seg_w);
-    const int f0 = max(0, cc0 - a.st_halo) & ~3;
-    const int gj0 = f0 + CPL * lane;
+    // column geometry of the first row's segment (the only one without GEN)
+    const SegGeo g0 = seg_geo<GEN>(a, rm.pl0);
+    const int cc0 = g0.cc0, cc1 = g0.cc1;
+    const int gj0 = g0.f0 + CPL * lane;
     const bool lane_ok = gj0 < W;
-    const bool core = lane_ok && gj0 >= cc0 && gj0 < cc1;   // W % 4 == 0: a lane's 4 columns are all core or none
+    const bool core = lane_ok && gj0 >= cc0 && gj0 < cc1;   // a lane's 4 columns are all core or none
     const int nsteps = Q + 4 + 3 * n;
     // 16 waves always; waves beyond the pipeline (n < 10) only keep the barrier count
     const int role = (w < SP_FRONT) ? 0 : (w < SP_FRONT + n ? 1 : (w < SP_FRONT + n + SP_BACK ? 2 : 3));
@@ -1032,6 +1069,8 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         uint32_t pq0 = 0, pq1 = 0, pq2 = 0, pq3 = 0;          // second quad (W % 4 != 0 rows)
         float zq0 = 0.f, zq1 = 0.f, zq2 = 0.f, zq3 = 0.f;
         int esh = 0;
+        int gjf = gj0;                                      // first column of the lane in row q (GEN:
+        bool okf = lane_ok;                                 // per column segment)
         const float* xin = a.x[par_in];
         const float* u2in = a.u2[par_in];
         const float* x2in = ALPHA1 ? nullptr : a.x2[par_in];
@@ -1048,19 +1087,21 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
 #endif
             const int rr = min(rc.r, H - 1);
             const int bi = (q >> 2) & 1;
-            const int bb = rc.p / C;
-            const size_t base = plane_off(rc.p) + (size_t)rr * L + gjc;
+            const SegGeo g = seg_geo<GEN>(a, rc.p);
+            const int gjr = GEN ? min(g.f0 + CPL * lane, L - CPL) : gjc;
+            const int bb = g.rp / C;
+            const size_t base = plane_off(g.rp) + (size_t)rr * L + gjr;
             if (part == 0) {
                 glds16(xin + base, &sh.fst[fw][bi][0][0]);
             } else if (part == 1) {
-                glds16(a.yobs + (size_t)bb * a.y_cs + (size_t)(rc.p - bb * C) * HW + (size_t)rr * L + gjc,
+                glds16(a.yobs + (size_t)bb * a.y_cs + (size_t)(g.rp - bb * C) * HW + (size_t)rr * L + gjr,
                        &sh.fst[fw][bi][1][0]);
             } else if (part == 2) {
                 glds16(u2in + 2 * base, &sh.fst[fw][bi][2][0]);
                 glds16(u2in + 2 * base + 4, &sh.fst[fw][bi][3][0]);
             } else {
                 if (!ALPHA1) glds16(x2in + base, &sh.fst[fw][bi][4][0]);
-                glds4(a.mask + (size_t)bb * a.m_cs + (size_t)rr * L + gjc, &sh.fmk[fw][bi][0]);
+                glds4(a.mask + (size_t)bb * a.m_cs + (size_t)rr * L + gjr, &sh.fmk[fw][bi][0]);
             }
         };
         // row fw's loads up front; afterwards the loads of row q + 4 are issued one part per
@@ -1079,16 +1120,21 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                 if (q >= 0 && q < Q) {
                     if (p < 3) front_issue(p, q + 4, rc_dma);
                     if (p == 0) {
-                        const int bb = rc_cur.p / C, cc = rc_cur.p - bb * C;
+                        const SegGeo g = seg_geo<GEN>(a, rc_cur.p);
+                        const int bb = g.rp / C, cc = g.rp - bb * C;
+                        if (GEN) {                                  // this row's segment's lanes
+                            gjf = g.f0 + CPL * lane;
+                            okf = gjf < W;
+                        }
                         // element index in the chain's unpadded C*H*W image: the noise stream
                         // does not depend on the row pitch
-                        const size_t e = ((size_t)cc * H + rc_cur.r) * W + gj0;
+                        const size_t e = ((size_t)cc * H + rc_cur.r) * W + gjf;
                         esh = (int)(e & 3);                         // the same for every lane of the row
                         uint32_t c0 = (uint32_t)(e >> 2), c1 = (uint32_t)step, c2 = TAG_LANGEVIN,
                                  c3 = (uint32_t)(a.seed >> 32);
                         philox4x32_10(c0, c1, c2, c3, (uint32_t)a.seed, (uint32_t)(a.chain0 + bb));
                         ph0 = c0; ph1 = c1; ph2 = c2; ph3 = c3;
-                        if (GENW && esh != 0) {                     // the lane's 4 elements span two quads
+                        if (GEN && esh != 0) {                     // the lane's 4 elements span two quads
                             uint32_t d0 = (uint32_t)(e >> 2) + 1u, d1 = (uint32_t)step, d2 = TAG_LANGEVIN,
                                      d3 = (uint32_t)(a.seed >> 32);
                             philox4x32_10(d0, d1, d2, d3, (uint32_t)a.seed, (uint32_t)(a.chain0 + bb));
@@ -1096,10 +1142,10 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                         }
                     } else if (p == 1) {
                         box_muller(ph0, ph1, zn0, zn1);
-                        if (GENW && esh != 0) box_muller(pq0, pq1, zq0, zq1);
+                        if (GEN && esh != 0) box_muller(pq0, pq1, zq0, zq1);
                     } else if (p == 2) {
                         box_muller(ph2, ph3, zn2, zn3);
-                        if (GENW && esh != 0) {
+                        if (GEN && esh != 0) {
                             box_muller(pq2, pq3, zq2, zq3);
                             // element i of the lane = output (esh + i) of the two-quad window
                             const float w8[8] = {zn0, zn1, zn2, zn3, zq0, zq1, zq2, zq3};
@@ -1130,17 +1176,17 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                         for (int k = 0; k < CPL; ++k) {
                             if (EXACT) {
                                 const float g = (-mk[k] * (X[k] - yo[k])) / a.sigma2;
-                                Yv[k] = lane_ok ? (X[k] + a.c1 * g) + a.c2 * Z[k] : 0.f;
+                                Yv[k] = okf ? (X[k] + a.c1 * g) + a.c2 * Z[k] : 0.f;
                             } else {
                                 const float g = (mk[k] * (yo[k] - X[k])) * a.inv_sigma2;
-                                Yv[k] = lane_ok ? __builtin_fmaf(a.c2, Z[k], __builtin_fmaf(a.c1, g, X[k])) : 0.f;
+                                Yv[k] = okf ? __builtin_fmaf(a.c2, Z[k], __builtin_fmaf(a.c1, g, X[k])) : 0.f;
                             }
                         }
                         const float4 Y4 = make_float4(Yv[0], Yv[1], Yv[2], Yv[3]);
                         float4 x2s;
                         if (fresh) x2s = Y4;
                         else x2s = ALPHA1 ? fX : fXS;
-                        if (!lane_ok) x2s = zero4;
+                        if (!okf) x2s = zero4;
                         const int s0 = q & 1;
                         STAMP_SEG(stp, 1);
                         sh.x2[0][s0][lane] = x2s;
@@ -1165,8 +1211,8 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         const int lastk = W - 1 - gj0;                    // in 0..3 on the lane holding column W-1
         const int nreal = min(CPL, max(0, W - gj0));      // real (non-pitch-padding) columns of the lane
         __builtin_amdgcn_s_setprio(1);
-        if (trk) stage_loop<EXACT, true, GENW>(a, sh, rm, k_st, nsteps, lane, lastk, nreal, core, stp);
-        else stage_loop<EXACT, false, GENW>(a, sh, rm, k_st, nsteps, lane, lastk, nreal, core, stp);
+        if (trk) stage_loop<EXACT, true, GEN>(a, sh, rm, k_st, nsteps, lane, lastk, nreal, core, stp);
+        else stage_loop<EXACT, false, GEN>(a, sh, rm, k_st, nsteps, lane, lastk, nreal, core, stp);
     } else if (role == 3) {
         for (int t = 0; t < nsteps; ++t) step_barrier(stp);
     } else {
@@ -1195,7 +1241,9 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
             if (need_prev) {
                 const int rr = min(rc.r, H - 1);
                 const int bi = (q >> 1) & 1;
-                const size_t base = plane_off(rc.p) + (size_t)rr * L + gjc;
+                const SegGeo g = seg_geo<GEN>(a, rc.p);
+                const int gjr = GEN ? min(g.f0 + CPL * lane, L - CPL) : gjc;
+                const size_t base = plane_off(g.rp) + (size_t)rr * L + gjr;
                 glds16(mean_in + base, &sh.bst[bw][bi][0][0]);
                 glds16(sq_in + base, &sh.bst[bw][bi][1][0]);
             }
@@ -1203,11 +1251,11 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         // vector-memory stores per core row (all lanes of a wave store together; lane 0 is core)
         const int nst = 3 + (ALPHA1 ? 0 : 1) + ((si.acc && (si.blockend || si.liveout)) ? 2 : 0) + (si.sample ? 1 : 0);
         // a row's stores are spread over the wave's two steps: state + accumulators, then the rest
-        bool hold = false;
+        bool hold = false, hcore = core;
         size_t h_base = 0;
         float4 hM = zero4, hQ = zero4, hX = zero4;
         auto flush_held = [&]() {
-            if (!core) return;
+            if (!(GEN ? hcore : core)) return;
             if (si.acc) {
                 if (si.blockend) {
                     st_nt(a.blocks + (size_t)si.blk * BE + h_base, hM);
@@ -1281,8 +1329,12 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                         c1 = c2 + 2 + ns;
                         c2 = ns;
                     }
-                    if (rowcore && core) {
-                        const size_t base = plane_off(rc.p) + (size_t)rc.r * L + gj0;
+                    // GEN: the lanes' columns of this row's segment
+                    const SegGeo gr = seg_geo<GEN>(a, rc.p);
+                    const int gjr = GEN ? gr.f0 + CPL * lane : gj0;
+                    const bool corer = GEN ? (gjr < W && gjr >= gr.cc0 && gjr < gr.cc1) : core;
+                    if (rowcore && corer) {
+                        const size_t base = plane_off(gr.rp) + (size_t)rc.r * L + gjr;
                         st_nt(a.x[par_out] + base, Xo);
                         float* u2o = a.u2[par_out] + 2 * base;
                         st_nt(u2o, make_float4(U0.x, U1.x, U0.y, U1.y));
@@ -1292,6 +1344,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                         h_base = base; hM = M4; hQ = Q4; hX = Xo;
                     }
                     hold = rowcore;
+                    if (GEN) hcore = corer;
                 } else if (hold) {
                     flush_held();
                     hold = false;
@@ -1315,7 +1368,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
     // early-stop test, per chain); the tracking stages wrote sh.red[segment][k - 1]
 }
 
-template <bool EXACT, bool ALPHA1, bool GENW>
+template <bool EXACT, bool ALPHA1, bool GEN>
 __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     __shared__ StreamShared sh;
     __shared__ int s_stop[MAXG];
@@ -1332,8 +1385,7 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     {
         RowMap rm;
         build_rowmap(a, blockIdx.x, rm);
-        const int cseg = a.split_wgs > 0 ? 0 : blockIdx.x - (blockIdx.x / a.st_nsegs) * a.st_nsegs;
-        stream_pass<EXACT, ALPHA1, GENW>(a, sh, rm, a.n_tv, cseg, true, step, fresh, stp);
+        stream_pass<EXACT, ALPHA1, GEN>(a, sh, rm, a.n_tv, true, step, fresh, stp);
         if (!a.fin_inline) return;        // main-pass-only launch (kernel timing): no side effects
         // rel_err partial sums of this stream -> global, per segment's chain (deepinv's
         // early-stop test, per chain); the tracking stages wrote sh.red[segment][k - 1]
@@ -1341,7 +1393,7 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
         for (int tt = threadIdx.x; tt < SP_MAXSEG * SP_MAXST; tt += blockDim.x) {
             const int sg = tt / SP_MAXST, it = tt - sg * SP_MAXST;     // it = k - 1
             if (sg < rm.ns && it >= 2 && it <= a.n_tv - 2) {
-                const int pl = rm.pl(sg);
+                const int pl = rm.pl(sg) / a.st_nsegs;        // virtual plane -> plane
                 const int g = a.per_chain_norm ? pl / C : 0;
                 atomicAdd(&a.norms[((size_t)g * a.n_tv + it) * 2], (double)sh.red[sg][it][0]);
                 atomicAdd(&a.norms[((size_t)g * a.n_tv + it) * 2 + 1], (double)sh.red[sg][it][1]);
@@ -1404,9 +1456,9 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
         if (item < 0) break;
         const int plane = item / a.st_nsegs;
         RowMap rm;
-        plane_rowmap(a.H, plane, rm);
+        plane_rowmap(a.H, item, rm);                 // the virtual plane (plane, column segment)
         const int nstop = __builtin_amdgcn_readfirstlane(s_stop[plane / C]);
-        stream_pass<EXACT, ALPHA1, GENW>(a, sh, rm, nstop, item - plane * a.st_nsegs, false, step, fresh, stp);
+        stream_pass<EXACT, ALPHA1, GEN>(a, sh, rm, nstop, false, step, fresh, stp);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < a.B * a.n_tv * 2; i += blockDim.x) a.norms[i] = 0.0;
@@ -1942,18 +1994,17 @@ static int device_cus() {
 // Row-split workgroup count for the streaming kernel (0 = one workgroup per plane).
 // req: 0 auto, -1 per plane, > 0 forced.  A range of R rows touches at most ceil(R/H) + 1
 // planes, so R <= 3H keeps it within SP_MAXSEG = 4 segments: G >= ceil(P/3).
-static int choose_split(int B, int C, int H, int W, int h, int req, int* out) {
-    const long long P = (long long)B * C, T = P * H;
+// P: (virtual) planes = B * C * column segments, each of H rows
+static int choose_split(long long P, int H, int h, int req, int* out) {
+    const long long T = P * H;
     const long long gmin = (P + SP_MAXSEG - 2) / (SP_MAXSEG - 1);
     *out = 0;
     if (req < 0) return 0;
     if (req > 0) {
-        if (W > TV_COLS) return fail(0, "psgla_tv_step: stream_wgs > 0 needs W <= 256");
-        if (req < gmin || req > T) return fail(0, "psgla_tv_step: stream_wgs outside [ceil(B*C/3), B*C*H]");
+        if (req < gmin || req > T) return fail(0, "psgla_tv_step: stream_wgs outside [ceil(P/3), P*H]");
         *out = req;
         return 0;
     }
-    if (W > TV_COLS) return 0;
     const long long cus = device_cus();
     if (P > (SP_MAXSEG - 1) * cus) return 0;          // enough planes: one workgroup each
     long long g = (T + 4LL * h - 1) / (4LL * h);      // >= 4 n_tv core rows per range
@@ -1994,11 +2045,9 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
     if (mask & 1) {
         if (FRONT == FRONT_INPAINT && a.stream) {
             TvArgs s = a;
-            s.st_halo = a.n_tv;
-            s.st_nsegs = stream_segments(a.W, a.ldw, a.n_tv, &s.st_seg_w);
             s.fin_inline = (mask & 2) ? 1 : 0;
-            const int grid = s.split_wgs > 0 ? s.split_wgs : P * s.st_nsegs;
-            if (s.ldw == s.W)
+            const int grid = s.split_wgs > 0 ? s.split_wgs : P * s.st_nsegs;   // virtual planes
+            if (s.ldw == s.W && s.st_nsegs == 1)
                 hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1, false>), dim3(grid), dim3(TV_THREADS), 0, st, s);
             else
                 hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1, true>), dim3(grid), dim3(TV_THREADS), 0, st, s);
@@ -2075,8 +2124,12 @@ int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream) {
     if (d->kernel_variant == 2 && !streamable) return fail(0, "psgla_tv_step: shape not supported by the streaming kernel");
     if (!a.stream && a.ldw != a.W) return fail(0, "psgla_tv_step: a row pitch ldw != W needs the streaming kernel");
     a.split_wgs = 0;
+    a.st_nsegs = 1;
     if (a.stream) {
-        const int rc = choose_split(d->B, d->C, d->H, a.ldw, d->n_tv, d->stream_wgs, &a.split_wgs);
+        a.st_halo = d->n_tv;
+        a.st_nsegs = stream_segments(a.W, a.ldw, d->n_tv, &a.st_seg_w);
+        const int rc = choose_split((long long)d->B * d->C * a.st_nsegs, d->H, d->n_tv, d->stream_wgs,
+                                    &a.split_wgs);
         if (rc) return rc;
     }
     hipStream_t st = (hipStream_t)stream;

@@ -524,3 +524,50 @@ def test_psgla_padded_rows_returns_reference_shapes():
             np.testing.assert_array_equal(u.cpu().numpy(), v.numpy())
     assert tuple(den.x2.shape) == (1, 3, 21, 37) and den.x2.is_contiguous()
     assert tuple(den.u2.shape) == (1, 3, 21, 37, 2)
+
+
+@pytest.mark.parametrize("W,stream_wgs", [(301, 0), (301, 4), (301, 7), (301, 33), (483, 0), (483, 9), (300, 6)])
+def test_stream_segmented_row_split_exact_vs_oracle(W, stream_wgs):
+    """W > 256: rows of every (plane, column segment) pair cut into ranges over the CUs (ranges
+    crossing segment and plane boundaries, n_tv halo rows at cuts): bit-identical to the checker."""
+    B, H, n_iter = 2, 20, 10
+    eng, (dg, y, init, mask2d, c1, c2) = _fused_batch(B, 7, exact=True, n_iter=n_iter, H=H, W=W,
+                                                      variant="stream", stream_wgs=stream_wgs)
+    eng.run(n_iter, graph_steps=0)
+    torch.cuda.synchronize()
+    bm, bm2 = eng.blocks()
+    for b in range(B):
+        tv = orc.TVDenoiser(n_it_max=10)
+        Xl, Ml, M2l = orc.psgla(init, dg, tv, torch.tensor(1.0), torch.tensor(10.0), sig_float=10 / 255.0,
+                                delta=(10 / 255.0) ** 2, n_iter=n_iter, n_inter=5, n_inter_mmse=4, seed=3,
+                                chain=7 + b)
+        np.testing.assert_array_equal(eng.samples()[:, b].cpu().numpy(), np.stack([t.numpy() for t in Xl]))
+        np.testing.assert_array_equal(bm[:, b].cpu().numpy(), np.stack([t.numpy() for t in Ml]))
+        np.testing.assert_array_equal(eng.u2_state[b].cpu().numpy(), tv.u2.numpy()[0])
+
+
+def test_stream_segmented_early_stop_exact_vs_oracle():
+    """Early stop with padded rows and column segments: the last workgroup re-streams every
+    (plane, segment) of the stopped chains -- bit-identical."""
+    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    B, H, W, n_iter, tol = 2, 18, 263, 10, 3e-2
+    g = torch.Generator().manual_seed(9)
+    x = torch.rand((1, 3, H, W), generator=g)
+    dg, y, init, mask2d = orc.inpainting_problem(x, seed_ip=3)
+    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
+    eng = FusedTvChains(init.expand(B, -1, -1, -1).contiguous().to(DEV), y.to(DEV), mask2d.to(torch.uint8).to(DEV),
+                        c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)), alpha=1.0,
+                        ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10, tol=tol), seed=4,
+                        n_iter=n_iter, n_inter=3, n_inter_mmse=2, exact=True, kernel_variant="stream")
+    eng.run(n_iter, graph_steps=0)
+    torch.cuda.synchronize()
+    fired = False
+    for b in range(B):
+        tv = _RecordingTV(n_it_max=10, tol=tol)
+        Xl, Ml, M2l = orc.psgla(init, dg, tv, torch.tensor(1.0), torch.tensor(10.0), sig_float=10 / 255.0,
+                                delta=(10 / 255.0) ** 2, n_iter=n_iter, n_inter=3, n_inter_mmse=2, seed=4, chain=b)
+        fired = fired or min(tv.its) < 10
+        np.testing.assert_array_equal(eng.samples()[:, b].cpu().numpy(), np.stack([t.numpy() for t in Xl]))
+        np.testing.assert_array_equal(eng.u2_state[b].cpu().numpy(), tv.u2.numpy()[0])
+    assert fired, "test needs the early stop to fire"
