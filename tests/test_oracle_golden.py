@@ -58,11 +58,14 @@ def test_radius_and_angle_tables_are_sane():
     assert np.max(np.abs(c - np.cos(th))) < 2e-7 and np.max(np.abs(s - np.sin(th))) < 2e-7
 
 
-def _chk(out, fx):
+def _chk(out, fx, rtol=None):
     Xl, Ml, M2l = out
-    np.testing.assert_array_equal(np.stack([t.numpy() for t in Xl]), fx["samples"])
-    np.testing.assert_array_equal(np.stack([t.numpy() for t in Ml]), fx["blocks"])
-    np.testing.assert_array_equal(np.stack([t.numpy() for t in M2l]), fx["blocks2"])
+    for got, key in ((Xl, "samples"), (Ml, "blocks"), (M2l, "blocks2")):
+        a = np.stack([t.numpy() for t in got])
+        if rtol is None:
+            np.testing.assert_array_equal(a, fx[key])
+        else:
+            np.testing.assert_allclose(a, fx[key], rtol=rtol, atol=rtol)
 
 
 def test_inpainting_setup_matches_reference():
@@ -138,7 +141,9 @@ def test_psgla_relaxation_alpha03():
     out = orc.psgla(init, dg, den, torch.tensor(alpha, dtype=torch.float32),
                     torch.tensor(lam, dtype=torch.float32), sig_float=s, delta=delta, n_iter=int(n),
                     n_inter=int(ni), n_inter_mmse=int(nm), seed=int(seed))
-    _chk(out, fx)
+    # torch's CPU conv2d (oneDNN) picks its accumulation order by host ISA, so the conv prior is
+    # only reproducible to fp32 rounding across machines: north_star tolerance (1e-5 relative).
+    _chk(out, fx, rtol=1e-5)
 
 
 def test_reference_error_behaviour():
