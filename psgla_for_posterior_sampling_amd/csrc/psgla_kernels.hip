@@ -908,7 +908,7 @@ __device__ __forceinline__ void stage_phase_b(const TvArgs& a, const StageRow& r
 // the rel-err partial sums are flushed per segment (different segments may be different chains).
 template <bool EXACT, bool TRK, bool GEN>
 __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, const RowMap& rm, int k, int nsteps,
-                                           int lane, int lastk, int nreal, bool core, Stamps& stp) {
+                                           int Qk, int lane, int lastk, int nreal, bool core, Stamps& stp) {
     // GEN: the lane's columns change with the column segment of the row (row split over virtual
     // planes): lastk / nreal / core follow the primal row's segment; each row carries its lastk
     // to its dual (StageRow.lk)
@@ -921,7 +921,7 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
             core = gj < a.W && gj >= g.cc0 && gj < g.cc1;
         }
     };
-    const int Q = rm.Q;
+    const int Q = Qk;                    // rows this stage runs (the stream's, bottom-halo trimmed)
     const int tbeg = 1 + 3 * k;          // step of lookahead row 0
     StageRow RA, RB, RC;
     const float zero[CPL] = {0.f, 0.f, 0.f, 0.f};
@@ -1053,7 +1053,14 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
     const int gj0 = g0.f0 + CPL * lane;
     const bool lane_ok = gj0 < W;
     const bool core = lane_ok && gj0 >= cc0 && gj0 < cc1;   // a lane's 4 columns are all core or none
-    const int nsteps = Q + 4 + 3 * n;
+    // Bottom-halo trim (split mode): the stream's last row is an artificial edge, so stage k's
+    // output is exact down to one row less than its input's; the core rows (< Qb) only need
+    // stage k to run rows 0 .. Qb + n - k, and the back none of the halo rows.  The pipeline
+    // drains hbot - 1 steps earlier (no change without a bottom halo).
+    const int Qb = Q - rm.hbot;
+    auto stage_rows = [&](int k) { return min(Q, Qb + n - k + 1); };
+    int nsteps = max(Q + 4, Qb + 4 + 3 * n);
+    for (int k = 1; k <= n; ++k) nsteps = max(nsteps, stage_rows(k) + 3 + 3 * k);
     // 16 waves always; waves beyond the pipeline (n < 10) only keep the barrier count
     const int role = (w < SP_FRONT) ? 0 : (w < SP_FRONT + n ? 1 : (w < SP_FRONT + n + SP_BACK ? 2 : 3));
 
@@ -1211,8 +1218,9 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         const int lastk = W - 1 - gj0;                    // in 0..3 on the lane holding column W-1
         const int nreal = min(CPL, max(0, W - gj0));      // real (non-pitch-padding) columns of the lane
         __builtin_amdgcn_s_setprio(1);
-        if (trk) stage_loop<EXACT, true, GEN>(a, sh, rm, k_st, nsteps, lane, lastk, nreal, core, stp);
-        else stage_loop<EXACT, false, GEN>(a, sh, rm, k_st, nsteps, lane, lastk, nreal, core, stp);
+        const int qk = stage_rows(k_st);
+        if (trk) stage_loop<EXACT, true, GEN>(a, sh, rm, k_st, nsteps, qk, lane, lastk, nreal, core, stp);
+        else stage_loop<EXACT, false, GEN>(a, sh, rm, k_st, nsteps, qk, lane, lastk, nreal, core, stp);
     } else if (role == 3) {
         for (int t = 0; t < nsteps; ++t) step_barrier(stp);
     } else {
@@ -1276,7 +1284,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         for (int t = 0; t < nsteps; ++t) {
                 // ======================= BACK =======================
                 const int q = t - 4 - 3 * n;
-                if (q >= 0 && q < Q && (q & 1) == bw) {
+                if (q >= 0 && q < Qb && (q & 1) == bw) {
                     const int sl = q & 1;
                     const float4 X2 = sh.x2[n][sl][lane];
                     const float4 U0 = sh.u0[n][sl][lane];
