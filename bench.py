@@ -145,13 +145,15 @@ def main():
     c1f = float((torch.tensor(delta).float() / torch.tensor(lam).float()).item())
     c2f = float((torch.tensor(np.sqrt(2)).float() * torch.tensor(s).float()).item())
     n_inter = nm = 10
-    n_iter = args.warmup + args.steps
+    gs = max(1, min(args.graph_steps, args.steps))
+    # steps the engine runs: eager warm-up + one graph replay (>= the W warm-up steps), the timed
+    # replays, the kernel-alone cross-check; n_iter only sizes the sample / block-mean buffers
+    n_iter = max(1, args.warmup - gs) + gs + (args.steps // gs) * gs + 8
     eng = FusedTvChains(init.contiguous(), y.contiguous(), mask_2d.to(torch.uint8), c1=c1f, c2=c2f,
                         sigma2=float(np.float32(sigma1 ** 2)), alpha=1.0, ths=float(np.float32(s)),
                         tv=K.TvConstants(n_it_max=args.tv_iters), seed=0, n_iter=n_iter + args.kernel_iters,
                         n_inter=n_inter, n_inter_mmse=nm, chain0=c0, exact=args.exact,
                         stream_wgs=args.stream_wgs, kernel_variant=args.variant)
-    gs = max(1, min(args.graph_steps, args.steps))
     # warm-up: eager steps + graph capture
     eng.step(max(1, args.warmup - gs))
     eng.capture(gs)
