@@ -195,6 +195,12 @@ int psgla_blur_grad(const float* X, const float* y, int64_t y_chain_stride, cons
 /* *d_step += 1 (one thread) */
 int psgla_advance_step(int64_t* d_step, void* stream);
 
+/* DnCNN conv epilogue (the deepinv DnCNN the reference loads, sampling_images.py:129-134, called at
+ * restoration_algorithms.py:238): y = relu(y + bias[c]) (relu != 0) or y + bias[c], in place, n
+ * elements.  Layout NHWC when hw == 0 (channel fastest, C % 4 == 0), NCHW with plane size hw
+ * (hw % 4 == 0) otherwise.  Same fp32 operations as PyTorch's bias add + clamp_min(0). */
+int psgla_bias_act(float* y, const float* bias, int64_t n, int32_t C, int64_t hw, int32_t relu, void* stream);
+
 /* Diagnostic (tests): Box-Muller radius r(k) and (cos, sin)(2 pi k 2^-24) of the noise stream for the
  * 24-bit indices k0 .. k0+n-1, so the GPU stream can be checked against the CPU checker exhaustively. */
 int psgla_debug_bm_tables(float* r, float* cs, float* sn, uint32_t k0, uint32_t n, void* stream);

@@ -78,6 +78,7 @@ _SIGNATURES = {
     "psgla_blur_grad": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32,
                                 c_f, c_f, c_f, c_u64, c_i32, c_vp, c_i64, c_i32, c_vp]),
     "psgla_advance_step": (c_i32, [c_vp, c_vp]),
+    "psgla_bias_act": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i64, c_i32, c_vp]),
     "psgla_debug_bm_tables": (c_i32, [c_vp, c_vp, c_vp, c_u32, c_u32, c_vp]),
 }
 

@@ -1892,6 +1892,30 @@ __global__ void pnpula_update_kernel(const float* X, const float* gp, const floa
     }
 }
 
+// DnCNN layer epilogue (denoisers.py DnCNN, deepinv's conv -> bias -> ReLU): y = relu(y + bias[c]) in
+// place, one pass instead of PyTorch's bias add and ReLU passes over a 1 GB activation tensor at 64
+// chains.  NHWC (hw == 0: c = e % C, C % 4 == 0) or NCHW (c = (e / hw) % C, hw % 4 == 0).  ReLU as
+// (v < 0) ? 0 : v -- PyTorch's clamp_min(0): NaN and -0 pass through unchanged.
+__global__ void bias_act_kernel(float* y, const float* bias, long long n4, int C, long long hw, int relu) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+        const long long e = 4 * i;
+        float4 v = ld4(y + e);
+        float4 bb;
+        if (hw == 0) {
+            bb = ld4(bias + (int)(e % C));
+        } else {
+            const float b1 = bias[(int)((e / hw) % C)];
+            bb = make_float4(b1, b1, b1, b1);
+        }
+        v.x = v.x + bb.x; v.y = v.y + bb.y; v.z = v.z + bb.z; v.w = v.w + bb.w;
+        if (relu) {
+            v.x = v.x < 0.f ? 0.f : v.x; v.y = v.y < 0.f ? 0.f : v.y;
+            v.z = v.z < 0.f ? 0.f : v.z; v.w = v.w < 0.f ? 0.f : v.w;
+        }
+        st4(y + e, v.x, v.y, v.z, v.w);
+    }
+}
+
 // g = ((-m) (X - y)) / sigma2   (sampling_images.py:295)
 __global__ void inpaint_grad_kernel(const float* X, const float* y, long long y_cs, const uint8_t* mask,
                                     long long m_cs, float* g, int B, int C, int H, int W, float sigma2) {
@@ -2286,6 +2310,19 @@ int psgla_debug_bm_tables(float* r, float* cs, float* sn, uint32_t k0, uint32_t 
     if (!r || !cs || !sn) return fail(0, "psgla_debug_bm_tables: null");
     hipLaunchKernelGGL(bm_tables_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, r, cs, sn, k0, n);
     return launch_check("bm_tables");
+}
+
+int psgla_bias_act(float* y, const float* bias, int64_t n, int32_t C, int64_t hw, int32_t relu, void* stream) {
+    if (!y || !bias || n < 0 || C <= 0 || hw < 0) return fail(0, "psgla_bias_act: bad arguments");
+    if (n % 4 != 0) return fail(0, "psgla_bias_act: element count must be a multiple of 4");
+    if (hw == 0 && C % 4 != 0) return fail(0, "psgla_bias_act: NHWC needs C % 4 == 0");
+    if (hw > 0 && hw % 4 != 0) return fail(0, "psgla_bias_act: NCHW needs H*W % 4 == 0");
+    if (n == 0) return 0;
+    const long long n4 = n / 4;
+    const long long grid = (n4 + 255) / 256 < 256LL * 32 ? (n4 + 255) / 256 : 256LL * 32;
+    hipLaunchKernelGGL(bias_act_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, y, bias, n4, C,
+                       (long long)hw, relu);
+    return launch_check("bias_act");
 }
 
 int psgla_advance_step(int64_t* d_step, void* stream) {

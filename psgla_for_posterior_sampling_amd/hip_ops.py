@@ -158,6 +158,24 @@ def pnpula_update(X, gp, gd, X_out, delta: float, lambd: float, brw: float, c_mi
     return X_out
 
 
+def bias_act_(y: torch.Tensor, bias: torch.Tensor, relu: bool = True) -> torch.Tensor:
+    """In place y = relu(y + bias[c]) (or y + bias[c]) for an (N, C, H, W) conv output in NHWC
+    (channels_last) or NCHW memory; the DnCNN layer epilogue (one HBM pass instead of two)."""
+    N_, C, H, W = y.shape
+    if y.is_contiguous(memory_format=torch.channels_last) and C % 4 == 0:
+        hw = 0
+        ptr = y.data_ptr()
+        if y.dtype != torch.float32 or not y.is_cuda:
+            raise TypeError("bias_act_: y must be a CUDA float32 tensor")
+    else:
+        hw = H * W
+        ptr = _ptr(y, name="y")
+    b = bias.contiguous()
+    N.check(N.lib().psgla_bias_act(ptr, _ptr(b, name="bias"), y.numel(), C, hw, 1 if relu else 0, _stream()),
+            "psgla_bias_act")
+    return y
+
+
 def inpaint_grad(X, y, mask_u8, sigma2: float, out=None):
     """g = ((-m)(X - y)) / sigma2 with mask (H,W) or (B,H,W) uint8 and y (B|1,C,H,W)."""
     B, C, H, W = X.shape

@@ -157,3 +157,43 @@ def test_denoiser_chains_independent_of_batch_split():
     for f, a, b in zip(full, lo, hi):
         for u, v, w in zip(f, a, b):
             assert torch.equal(u, torch.cat([v, w], 0))
+
+
+@pytest.mark.parametrize("channels_last", [True, False])
+@pytest.mark.parametrize("relu", [True, False])
+def test_bias_act_bitwise_vs_torch(channels_last, relu):
+    """hip_ops.bias_act_ (the DnCNN layer epilogue) == PyTorch's bias add (+ ReLU), bit for bit,
+    NHWC and NCHW, including zeros, negative zeros and large values."""
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    g = torch.Generator(device=DEV).manual_seed(3)
+    y = torch.randn((3, 64, 20, 28), generator=g, device=DEV) * 5
+    y[0, :, 0, :4] = 0.0
+    y[1, :, 1, :4] = -0.0
+    b = torch.randn(64, generator=g, device=DEV)
+    b[:8] = 0.0
+    if channels_last:
+        y = y.contiguous(memory_format=torch.channels_last)
+    ref = y + b.view(1, -1, 1, 1)
+    if relu:
+        ref = torch.relu(ref)
+    out = K.bias_act_(y.clone(memory_format=torch.preserve_format), b, relu=relu)
+    assert torch.equal(out, ref)
+    assert torch.equal(torch.signbit(out), torch.signbit(ref))
+
+
+def test_dncnn_fused_epilogue_equals_torch_layers():
+    """DnCNN forward with the HIP bias+ReLU epilogue vs the same module run layer by layer in
+    PyTorch (conv with bias, then ReLU) on the GPU.  Not bitwise: MIOpen may pick another solver
+    (another summation order) for a convolution without bias, so fp32 tolerance."""
+    from psgla_for_posterior_sampling_amd.denoisers import DnCNN
+    torch.manual_seed(1)
+    m = DnCNN(depth=6, device=DEV)
+    x = torch.rand(2, 3, 32, 40, device=DEV)
+    with torch.no_grad():
+        out = m(x)
+        xc = x.contiguous(memory_format=torch.channels_last)
+        h = m.nl_list[0](m.in_conv(xc))
+        for i in range(m.depth - 2):
+            h = m.nl_list[i + 1](m.conv_list[i](h))
+        ref = (m.out_conv(h) + xc).contiguous()
+    assert rel(out.cpu().numpy(), ref.cpu().numpy()) < 1e-5
