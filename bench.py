@@ -1,25 +1,39 @@
 #!/usr/bin/env python3
 """Langevin-step throughput of the fused PSGLA+TV HIP step (BASELINE.json configs[1]).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 64] [--scaling weak|strong]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 64] [--scaling strong|weak]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Workload (config.workload): PSGLA, inpainting 50 %, TV denoiser (deepinv TVDenoiser,
 n_it_max=10, warm-started), s = 10/255, lambda = 10, delta = s^2, sigma = 1/255,
 n_inter = n_inter_mmse = 10 (the N = 10000 TV settings of sampling_images.py:180-198),
-synthetic 3x256x256 fp32 images (one per chain, U[0,1) from Philox seed 1234 + chain id),
-the reference's shared inpainting mask (torch.rand on the device generator, seed_ip = 0,
-> 0.5).  64 chains per GPU (weak scaling: chains are independent, no collective in the
-step; chain ids are global so results do not depend on the GPU count); one RCCL
-all_reduce after the timed region combines the per-chain MMSE PSNR.
+synthetic 3x256x256 fp32 images (one per chain, U[0,1) from the device generator seeded
+1234 + chain id), the reference's shared inpainting mask (torch.rand on the device
+generator, seed_ip = 0, > 0.5).
 
-Timed region: K steps replayed from a hipGraph (the device step counter advances the noise
-counter, block-mean coefficients and sample / block slots), barrier + synchronize on both
-sides, max over ranks.  value = chain-steps (image-steps of 3x256x256) per second over all
-GPUs.  The roofline figure divides the algorithmic bytes of one launch by the dominant kernel's
-(tv_stream_kernel: one launch per step) average duration from HIP events recorded on the replay
-stream around the timed region; the kernel re-launched alone on its own stream is reported beside
-it (kernel_ms_isolated) as a cross-check.
+Scaling: strong by default -- a batch of 64 chains in total, split
+contiguously over the N ranks (64/N chains per GPU); `--scaling weak` keeps 64 chains per GPU.
+Chains are independent: no collective in the step; chain ids are global, so every chain's
+samples are the same for any N.  One RCCL all_reduce after the timed region combines the
+per-chain MMSE PSNR.
+
+Timed region: exactly K steps (K // G hipGraph replays of G-step graphs + K % G eager launches;
+the device step counter advances the noise counter, block-mean coefficients and sample /
+block slots), barrier + synchronize on both sides, max over ranks.  value = chain-steps
+(image-steps of 3x256x256) per second over all GPUs.
+
+Warm-up: the W steps (eager + graph capture), then untimed graph replays until at least
+--warmup-seconds of GPU work have run (clocks and power state settle; reported as
+`warmup_s`), after which the step index is rewound to where the timed steps of a W-step
+warm-up would start -- the timed steps write the same sample / block slots as in a run that
+warmed up for W steps (the chain state simply continues).
+
+The roofline figure divides the algorithmic bytes of one launch by the dominant kernel's
+(tv_stream_kernel: one launch per step) average duration from HIP events recorded on the
+replay stream around the timed region; the kernel re-launched alone on its own stream is
+reported beside it (kernel_ms_isolated) as a cross-check.  `traffic` (HBM bytes per launch
+from rocprofv3 PMC counters) cannot be collected inside an un-profiled run: it is read from
+the committed profile named in `traffic_source`, measured at the commit it records.
 """
 from __future__ import annotations
 
@@ -37,6 +51,7 @@ sys.path.insert(0, REPO)
 
 METRIC = "Langevin steps/sec (3×256×256, batch=64) at 1/2/4/8 GPU; HBM GB/s vs roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PMC_PROFILE = os.path.join("profiles", "r02_pmc_tv_stream.json")
 
 
 def parse():
@@ -44,8 +59,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=400)
     p.add_argument("--warmup", type=int, default=40)
-    p.add_argument("--batch", type=int, default=64, help="chains per GPU (weak) or in total (strong)")
-    p.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    p.add_argument("--warmup-seconds", type=float, default=1.5,
+                   help="minimum untimed GPU work (graph replays) before the timed steps")
+    p.add_argument("--batch", type=int, default=64, help="chains in total (strong) or per GPU (weak)")
+    p.add_argument("--scaling", choices=["weak", "strong"], default="strong")
     p.add_argument("--H", type=int, default=256)
     p.add_argument("--W", type=int, default=256)
     p.add_argument("--graph-steps", type=int, default=20)
@@ -54,9 +71,10 @@ def parse():
     p.add_argument("--tv-iters", type=int, default=10, help="TV n_it_max (analysis only; the workload is 10)")
     p.add_argument("--stream-wgs", type=int, default=0, help="stream kernel work split (0 auto, -1 per plane)")
     p.add_argument("--variant", choices=["auto", "band", "stream"], default="auto", help="fused TV kernel (analysis)")
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the batch-1 CPU leg")
+    p.add_argument("--cpu-b64-steps", type=int, default=10, help="timed steps of the batch-64 CPU leg (0: skip)")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r01_pmc_tv_stream.json"))
+    p.add_argument("--pmc-json", default=os.path.join(REPO, PMC_PROFILE))
     return p.parse_args()
 
 
@@ -78,33 +96,68 @@ def algorithmic_bytes_per_launch(B, C, H, W, step0, steps, n_inter, nm):
     return tot / steps
 
 
-def cpu_baseline(seconds: float):
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(seconds: float, b64_steps: int):
     """The reference algorithm on the host cores: oracle/ (op-for-op torch-CPU restatement of
-    restoration_algorithms.py:231-271 + the deepinv TV prox), batch 1 as the reference runs."""
+    restoration_algorithms.py:231-271 + the deepinv TV prox, pinned to the reference by
+    tests/golden), at batch 1 (as the reference runs, bounded by `seconds`) and at batch 64
+    (the benched workload; `b64_steps` steps, one psgla call -- the reference needs n_iter >= 10)."""
     from oracle import psgla_oracle as orc
     threads = torch.get_num_threads()
-    g = torch.Generator().manual_seed(1234)
-    x = torch.rand((1, 3, 256, 256), generator=g)
-    dg, y, init, _ = orc.inpainting_problem(x, seed_ip=0)
     s = 10 / 255.0
-    tv = orc.TVDenoiser(n_it_max=10)
-    # time a bounded number of steps: run blocks of 10 steps until `seconds` have elapsed
-    steps = 0
-    t0 = time.perf_counter()
-    X = init
     alpha = torch.tensor(1.0)
     lam = torch.tensor(10.0)
-    while True:
-        Xl, _, _ = orc.psgla(X, dg, tv, alpha, lam, sig_float=s, delta=s ** 2, n_iter=10, n_inter=10,
+
+    def problem(B):
+        g = torch.Generator().manual_seed(1234)
+        x = torch.rand((B, 3, 256, 256), generator=g)
+        dg, y, init, _ = orc.inpainting_problem(x, seed_ip=0)
+        return dg, init
+
+    def run(B, n_iter, tv, X, dg):
+        Xl, _, _ = orc.psgla(X, dg, tv, alpha, lam, sig_float=s, delta=s ** 2, n_iter=n_iter, n_inter=10,
                              n_inter_mmse=10, seed=0)
-        X = Xl[-1][None]
+        return Xl[-1][None] if B == 1 else Xl[-1]
+
+    # batch 1: blocks of 10 steps until `seconds` have elapsed (the first block is warm-up)
+    dg, X = problem(1)
+    tv = orc.TVDenoiser(n_it_max=10)
+    X = run(1, 10, tv, X, dg)
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        X = run(1, 10, tv, X, dg)
         steps += 10
         if time.perf_counter() - t0 > seconds:
             break
-    dt = time.perf_counter() - t0
-    return {"value": steps / dt, "unit": "image-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} PSGLA+TV steps, batch 1, 3x256x256, torch-CPU oracle, {threads} threads, "
-                      f"{dt:.1f} s"}
+    dt1 = time.perf_counter() - t0
+    b1 = steps / dt1
+    out = {"value": round(b1, 2), "unit": "image-steps/s", "cores": threads, "kind": "port",
+           "sample": f"batch 1: {steps} PSGLA+TV steps (3x256x256) after 10 warm-up steps, {dt1:.1f} s",
+           "batch1_image_steps_per_s": round(b1, 2), "cpu_model": cpu_model(), "threads": threads,
+           "host_logical_cpus": os.cpu_count()}
+    if b64_steps > 0:
+        dg, X = problem(64)
+        tv = orc.TVDenoiser(n_it_max=10)
+        n = max(10, int(b64_steps))
+        t0 = time.perf_counter()
+        run(64, n, tv, X, dg)
+        dt = time.perf_counter() - t0
+        b64 = 64 * n / dt
+        out["batch64_image_steps_per_s"] = round(b64, 2)
+        out["batch64_ms_per_step"] = round(dt / n * 1e3, 1)
+        out["value"] = round(b64, 2)      # the benched workload's batch
+        out["sample"] = (f"batch 64: {n} PSGLA+TV steps (64x3x256x256, one psgla call, after the batch-1 leg) "
+                         f"in {dt:.1f} s; " + out["sample"])
+    return out
 
 
 def main():
@@ -125,6 +178,8 @@ def main():
 
     C, H, W = 3, args.H, args.W
     total_chains = args.batch * world if args.scaling == "weak" else args.batch
+    if total_chains < world:
+        raise SystemExit(f"{total_chains} chains cannot be split over {world} GPUs")
     c0, c1 = chain_range(total_chains, world, rank)
     B = c1 - c0
     # synthetic per-chain ground truths, the reference's shared mask, observations
@@ -145,29 +200,41 @@ def main():
     c1f = float((torch.tensor(delta).float() / torch.tensor(lam).float()).item())
     c2f = float((torch.tensor(np.sqrt(2)).float() * torch.tensor(s).float()).item())
     n_inter = nm = 10
-    gs = max(1, min(args.graph_steps, args.steps))
-    # steps the engine runs: eager warm-up + one graph replay (>= the W warm-up steps), the timed
-    # replays, the kernel-alone cross-check; n_iter only sizes the sample / block-mean buffers
-    n_iter = max(1, args.warmup - gs) + gs + (args.steps // gs) * gs + 8
+    # graphs of an even step count: rewinding the step index after the warm-up keeps the parity
+    gs = max(2, min(args.graph_steps, max(args.steps, 2)))
+    gs += gs & 1
+    w_eager = max(1, args.warmup - gs)
+    # steps the schedule is sized for: eager warm-up + one replay, the timed steps, the kernel-alone check
+    n_iter = w_eager + gs + args.steps + 8
     eng = FusedTvChains(init.contiguous(), y.contiguous(), mask_2d.to(torch.uint8), c1=c1f, c2=c2f,
                         sigma2=float(np.float32(sigma1 ** 2)), alpha=1.0, ths=float(np.float32(s)),
                         tv=K.TvConstants(n_it_max=args.tv_iters), seed=0, n_iter=n_iter + args.kernel_iters,
                         n_inter=n_inter, n_inter_mmse=nm, chain0=c0, exact=args.exact,
                         stream_wgs=args.stream_wgs, kernel_variant=args.variant)
-    # warm-up: eager steps + graph capture
-    eng.step(max(1, args.warmup - gs))
+    # warm-up: eager steps + graph capture + one replay
+    eng.step(w_eager)
     eng.capture(gs)
     eng.replay(1)
     torch.cuda.synchronize()
+    step0 = eng.steps_done
+    # time-based warm-up: replays until >= warmup_seconds of GPU work, then rewind the step index
+    tw0 = time.perf_counter()
+    n_warm = 0
+    while time.perf_counter() - tw0 < args.warmup_seconds:
+        for _ in range(5):
+            eng.replay(1)
+            eng.rewind(step0)
+            n_warm += gs
+        torch.cuda.synchronize()
+    warmup_s = time.perf_counter() - tw0
 
     def barrier():
         if world > 1:
             import torch.distributed as dist
             dist.barrier()
 
-    reps = args.steps // gs
-    steps = reps * gs
-    step0 = eng.steps_done
+    steps = args.steps
+    reps, rem = divmod(steps, gs)
     barrier()
     torch.cuda.synchronize()
     # HIP events on the stream the graphs (one tv_stream_kernel launch per step) are replayed on
@@ -176,6 +243,7 @@ def main():
     t0 = time.perf_counter()
     ev0.record()
     eng.replay(reps)
+    eng.step(rem)
     ev1.record()
     torch.cuda.synchronize()
     barrier()
@@ -206,16 +274,28 @@ def main():
     blocks, _ = eng.blocks()
     psnr_sum, n_chains = reduce_psnr(blocks, xs, world)
 
-    traffic = None
+    traffic, traffic_info = None, None
     if os.path.exists(args.pmc_json):
         try:
-            traffic = json.load(open(args.pmc_json)).get("hbm_bytes_per_launch")
+            pj = json.load(open(args.pmc_json))
+            if (pj.get("workload", {}).get("chains_per_gpu") in (None, B) and pj.get("exact", False) == args.exact
+                    and args.tv_iters == 10 and (H, W) == (256, 256)):
+                traffic = pj.get("hbm_bytes_per_launch")
+                traffic_info = {"traffic_source": os.path.relpath(args.pmc_json, REPO),
+                                "traffic_commit": pj.get("commit"),
+                                "traffic_note": "rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE), not measured in this run"}
         except Exception:
             traffic = None
 
     if rank == 0:
-        cpu = None if args.no_cpu else cpu_baseline(args.cpu_seconds)
+        cpu = None if args.no_cpu else cpu_baseline(args.cpu_seconds, args.cpu_b64_steps)
         value = total_chains * steps / dt
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": eng.main_kernel, "kernel_ms": round(live_kern_ms, 5),
+                "kernel_ms_isolated": round(kern_ms, 5), "algorithmic_bytes_per_launch": int(alg_bytes)}
+        if traffic_info:
+            roof.update(traffic_info)
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -223,6 +303,8 @@ def main():
             "n_gpus": world,
             "steps": steps,
             "warmup": args.warmup,
+            "warmup_s": round(warmup_s, 3),
+            "warmup_replayed_steps": n_warm,
             "ms_per_step": round(dt / steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": args.scaling,
@@ -233,12 +315,8 @@ def main():
                        "global_batch": total_chains, "chains_per_gpu": B, "image": [C, H, W],
                        "parallelism": f"chains{world}", "graph_steps": gs,
                        "kernel_mode": "exact" if args.exact else "fast",
-                       "batch_steps_per_s_per_gpu": round(steps / dt, 2)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": eng.main_kernel, "kernel_ms": round(live_kern_ms, 5),
-                         "kernel_ms_isolated": round(kern_ms, 5),
-                         "algorithmic_bytes_per_launch": int(alg_bytes)},
+                       "batch_steps_per_s": round(steps / dt, 2)},
+            "roofline": roof,
             "cpu_baseline": cpu,
             "mmse_psnr_mean_db": round(psnr_sum / max(n_chains, 1), 3),
         }

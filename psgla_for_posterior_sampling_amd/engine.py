@@ -152,6 +152,17 @@ class FusedTvChains:
             self.graph.replay()
             self.steps_done += self.graph_steps
 
+    def rewind(self, step: int):
+        """Set the step index (device counter, stream-ordered, and host count) back to `step`, which
+        must have the parity of the current step (the ping-pong state stays where it is).  For
+        benchmarking only: untimed warm-up replays can then run for any length of time and the timed
+        steps still write the sample / block slots of the schedule (the chain state simply continues)."""
+        step = int(step)
+        if step < 0 or (step - self.steps_done) % 2:
+            raise ValueError("rewind target must be >= 0 and of the current step's parity")
+        self.sched.d_step.fill_(step)
+        self.steps_done = step
+
     @property
     def main_kernel(self) -> str:
         """Name of the kernel psgla_tv_step dispatches for this shape (psgla_kernels.hip:

@@ -37,9 +37,14 @@ def main():
     p.add_argument("--round", default="r01")
     p.add_argument("--kernel", default="tv_stream_kernel")
     p.add_argument("--out", default=None)
+    p.add_argument("--commit", default=None, help="git commit the profiled tree was built from")
+    p.add_argument("--chains", type=int, default=64, help="chains per GPU of the profiled bench run")
+    p.add_argument("--exact", action="store_true", help="the profiled run used the exact kernel")
+    p.add_argument("--command", default=None, help="the profiled command")
     a = p.parse_args()
     c = load(a.dirs, a.kernel)
-    out = {"kernel": a.kernel, "counters_per_dispatch": c}
+    out = {"kernel": a.kernel, "counters_per_dispatch": c, "commit": a.commit, "exact": bool(a.exact),
+           "workload": {"chains_per_gpu": a.chains, "image": [3, 256, 256], "n_tv": 10}, "command": a.command}
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         fetch = 2.0 * c["FETCH_SIZE"] * 1024.0
         write = c["WRITE_SIZE"] * 1024.0
