@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PSGLA_HIP_ABI_VERSION 3
+#define PSGLA_HIP_ABI_VERSION 4
 
 /* Max inner TV iterations the fused (temporally blocked) kernel handles. */
 #define PSGLA_TV_MAX_FUSED_IT 24
@@ -68,10 +68,18 @@ typedef struct PsglaSchedule {
  * i.e.  Z ~ N(0,1);  Y = (X + c1*g(X)) + c2*Z;  X' = (1-alpha)*Y + alpha*TVprox(Y);
  *       accumulators / samples per PsglaSchedule.
  * State is double-buffered by step parity: step i reads x[i&1], u2[i&1], ...
- * and writes x[(i+1)&1], ...  Two kernels are launched: the fused tile kernel and
- * a small finaliser that honours deepinv's early stop (rel_err < tol at inner
- * iteration k >= 2, per chain: the affected chains are recomputed with k+1 inner
- * iterations), clears `fresh` and advances *d_step.
+ * and writes x[(i+1)&1], ...  deepinv's early stop (rel_err < tol at inner iteration
+ * k >= 2, per chain: the affected chains are recomputed with k+1 inner iterations)
+ * is honoured, `fresh` is cleared and *d_step advanced once the step is complete.
+ * What is launched depends on the variant the shape selects (kernel_variant 0):
+ *   - the row-streaming kernel (tv_stream_kernel: row pitch ldw % 4 == 0, 1 <= n_tv <= 10,
+ *     H >= 2, every width with column segments): ONE launch per step; its last
+ *     workgroup to finish evaluates the early stop, re-streams stopped chains and
+ *     advances the step (no second kernel);
+ *   - otherwise (n_tv > 10 or H < 2, or kernel_variant 1) the temporally blocked
+ *     band kernel (tv_main_kernel) followed by a small finaliser kernel
+ *     (tv_finalise_kernel, <= 8 workgroups) that does the same.
+ * launch_mask 1 launches only the main pass of either variant (timing).
  * ------------------------------------------------------------------------------- */
 typedef struct PsglaTvStep {
     int32_t B, C, H, W;
@@ -121,8 +129,15 @@ int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream);
 /* ---------------------------------------------------------------------------------
  * psgla_tv_prox: TVDenoiser.forward(y, ths) on a (B,C,H,W) tensor, deepinv 0.2.1
  * semantics: warm start from (x2_in, u2_in) unless `fresh`; early stop on the
- * relative change of the WHOLE tensor (as deepinv computes it).  Outputs x2_out,
- * u2_out (new buffers, like deepinv's out-of-place updates).
+ * relative change of the WHOLE tensor (as deepinv computes it), or of each chain
+ * (per_chain = 1: B independent reference runs, psgla's loop over a chain batch).
+ * Outputs x2_out, u2_out (new buffers, like deepinv's out-of-place updates).
+ * One call runs n_tv <= PSGLA_TV_MAX_FUSED_IT inner iterations; a longer
+ * n_it_max runs as consecutive calls ("chunks", hip_ops.tv_prox): chunk c has
+ * it0 = the global index of its first iteration (deepinv tests rel_err from
+ * global iteration 2 on), last_chunk = 1 on the final one, and reports in
+ * stopped[g] (device, [groups]) the iteration count after which group g stopped
+ * inside the chunk (0: it did not stop); the host then keeps that group's result.
  * ------------------------------------------------------------------------------- */
 typedef struct PsglaTvProx {
     int32_t B, C, H, W;
@@ -131,8 +146,12 @@ typedef struct PsglaTvProx {
     float* x2_out;       float* u2_out;
     float tau, one_plus_tau, sigma_tv, rho, ths, tol;
     int32_t n_tv, exact, fresh;
-    double* norms;            /* device [n_tv][2], zeroed */
+    double* norms;            /* device [groups][n_tv][2], zeroed (groups = B if per_chain else 1) */
     int32_t* arrive;          /* device int, zeroed       */
+    int32_t per_chain;        /* 1: early stop per chain (batch of independent chains)           */
+    int32_t it0;              /* global index of this call's first inner iteration (0 = whole call) */
+    int32_t last_chunk;       /* 1 (default use): no further chunk follows                         */
+    int32_t* stopped;         /* device [groups] or NULL: stop count inside this chunk, 0 = none   */
 } PsglaTvProx;
 
 int psgla_tv_prox(const PsglaTvProx* d, void* stream);
@@ -161,7 +180,8 @@ int psgla_relax_accumulate(const float* Y, const float* D, float* X, float alpha
  *   X = (1-alpha)*Y + alpha*D  (X = D when alpha_is_one; Y may then be NULL);
  *   samples / block accumulators of step i (PsglaSchedule, as psgla_relax_accumulate);
  *   Y_next = (X + c1*g(X)) + c2*Z_{i+1},  g = ((-m)*(X - y))/sigma2,  Z_{i+1} the noise of step i+1;
- *   X is stored only when X != NULL.  H*W % 4 == 0.  Identical to psgla_relax_accumulate +
+ *   X is stored only when X != NULL.  Any H, W (H*W % 4 != 0: a scalar variant over the chain's
+ *   element quads, same noise quads as psgla_langevin_update).  Identical to psgla_relax_accumulate +
  *   psgla_inpaint_grad + psgla_langevin_update, in one pass (28 B/elem at alpha = 1). */
 int psgla_relax_langevin_inpaint(const float* Y, const float* D, float* X, float alpha, int32_t alpha_is_one,
                                  const float* y, int64_t y_chain_stride, const uint8_t* mask,

@@ -11,7 +11,7 @@ import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PSGLA_LIB", os.path.join(_PKG, "libpsgla_hip.so"))
-ABI_VERSION = 3
+ABI_VERSION = 4
 TV_MAX_FUSED_IT = 24
 
 
@@ -55,6 +55,7 @@ class PsglaTvProx(ctypes.Structure):
         ("y", c_vp), ("x2_in", c_vp), ("u2_in", c_vp), ("x2_out", c_vp), ("u2_out", c_vp),
         ("tau", c_f), ("one_plus_tau", c_f), ("sigma_tv", c_f), ("rho", c_f), ("ths", c_f), ("tol", c_f),
         ("n_tv", c_i32), ("exact", c_i32), ("fresh", c_i32), ("norms", c_vp), ("arrive", c_vp),
+        ("per_chain", c_i32), ("it0", c_i32), ("last_chunk", c_i32), ("stopped", c_vp),
     ]
 
 

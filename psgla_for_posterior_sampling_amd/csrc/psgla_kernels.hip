@@ -73,6 +73,9 @@ struct TvArgs {
     int fresh_host;
     int* fresh_dev;
     int per_chain_norm;
+    int it0;                        // psgla_tv_prox chunks: global index of the first inner iteration
+    int last_chunk;                 // 1: the call's last chunk (a stop at its last iteration changes nothing)
+    int* stopped;                   // psgla_tv_prox chunks: [groups] stop count of the chunk (0: none)
     double* norms;
     int* arrive;
     int advance_step;
@@ -92,6 +95,11 @@ struct TvArgs {
     int fin_inline;                 // stream kernel: 1 = the last workgroup finalises the step
     unsigned long long* stamps;     // diagnostic build only (PSGLA_STAMPS): per-wave work/wait cycles
 };
+
+// Inner iterations (chunk-local) whose rel_err deepinv tests: global index >= 2 ("it > 1"); in the call's
+// last chunk not the last iteration (stopping there changes nothing)
+__device__ __forceinline__ int trk_lo(const TvArgs& a) { return a.it0 >= 2 ? 0 : 2 - a.it0; }
+__device__ __forceinline__ int trk_hi(const TvArgs& a) { return a.last_chunk ? a.n_tv - 2 : a.n_tv - 1; }
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float a, float b, float c, float d) {
@@ -302,7 +310,7 @@ __device__ __forceinline__ void tv_tile(const TvArgs& a, int plane, int tile, in
 
     // ------------------------------ inner TV iterations ------------------------------
     for (int it = 0; it < n_it; ++it) {
-        const bool trk = track && it >= 2 && it <= a.n_tv - 2;
+        const bool trk = track && it >= trk_lo(a) && it <= trk_hi(a);
         float sd = 0.f, sn = 0.f;
         // Phase A: x = prox_tau_fx(x2 - tau nabla^T u2, y); z = 2x - x2; x2 += rho (x - x2)
         const float4 up = (w > 0) ? urow[w - 1][lane] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -384,9 +392,9 @@ __device__ __forceinline__ void tv_tile(const TvArgs& a, int plane, int tile, in
     }
 
     // rel_err partial sums -> global (one fp64 atomic per iteration and workgroup)
-    if (track && n_it >= 4) {
+    if (track) {
         const int t = threadIdx.x;
-        if (t >= 2 && t <= a.n_tv - 2) {
+        if (t >= trk_lo(a) && t <= trk_hi(a) && t < n_it) {
             double sd = 0.0, sn = 0.0;
             for (int ww = 0; ww < TV_NW; ++ww) { sd += red[t][ww][0]; sn += red[t][ww][1]; }
             const int g = a.per_chain_norm ? b : 0;
@@ -480,21 +488,24 @@ __global__ void __launch_bounds__(TV_THREADS) tv_finalise_kernel(const TvArgs a)
     for (int g = threadIdx.x; g < G; g += blockDim.x) {
         // all partial norms of the chain in flight at once (one memory latency, not n_tv)
         double nd[MAXIT], nn[MAXIT];
+        const int tlo = trk_lo(a), thi = trk_hi(a);
 #pragma unroll
-        for (int t = 2; t < MAXIT; ++t) {
-            if (t <= a.n_tv - 2) {
+        for (int t = 0; t < MAXIT; ++t) {
+            if (t >= tlo && t <= thi) {
                 nd[t] = a.norms[((size_t)g * a.n_tv + t) * 2];
                 nn[t] = a.norms[((size_t)g * a.n_tv + t) * 2 + 1];
             }
         }
         int stop = a.n_tv;
+        bool found = false;
 #pragma unroll
-        for (int t = 2; t < MAXIT; ++t) {
-            if (t <= a.n_tv - 2 && stop == a.n_tv) {
+        for (int t = 0; t < MAXIT; ++t) {
+            if (t >= tlo && t <= thi && !found) {
                 const float rel = (float)sqrt(nd[t]) / (float)sqrt(nn[t]);
-                if (rel < a.tol) stop = t + 1;
+                if (rel < a.tol) { stop = t + 1; found = true; }
             }
         }
+        if (a.stopped && blockIdx.x == 0) a.stopped[g] = found ? stop : 0;
         s_stop[g] = stop;
         if (stop < a.n_tv) atomicOr(&s_flag, 1);
     }
@@ -1851,6 +1862,40 @@ __global__ void relax_langevin_inpaint_kernel(const float* Y, const float* D, fl
     }
 }
 
+// The same pass for H*W % 4 != 0 (set1c / CBSD68 are 481 x 321): chain-linear quads, so the noise
+// quad of an element is the one psgla_langevin_update gives it (e >> 2 of the chain's C*H*W image);
+// scalar loads, one element at a time.  grid: (quads of a chain, chain)
+__global__ void relax_langevin_inpaint_any_kernel(const float* Y, const float* D, float* X_out, float alpha,
+                                                  int alpha1, const float* y, long long y_cs, const uint8_t* mask,
+                                                  long long m_cs, float* Y_next, int B, int C, int H, int W,
+                                                  float sigma2, float c1, float c2, unsigned long long seed,
+                                                  int chain0, float* mean, float* sq, AccArgs s) {
+    const long long step = read_step(s.d_step, s.off);
+    const long long HW = (long long)H * W;
+    const long long E = (long long)C * HW;
+    const size_t BE = (size_t)B * E;
+    const int b = blockIdx.y;
+    const float* yp = y + (size_t)b * y_cs;
+    const uint8_t* mp = mask + (size_t)b * m_cs;
+    const long long Q = (E + 3) >> 2;
+    for (long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x; q < Q; q += (long long)gridDim.x * blockDim.x) {
+        float z[4];
+        normal_quad(seed, (uint32_t)(chain0 + b), (uint32_t)(step + 1), TAG_LANGEVIN, (uint32_t)q, z);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const long long e = 4 * q + j;
+            if (e >= E) break;
+            const size_t idx = (size_t)b * E + e;
+            const float x = alpha1 ? D[idx] : (1.0f - alpha) * Y[idx] + alpha * D[idx];
+            if (X_out) X_out[idx] = x;
+            acc_elem(s, step, idx, BE, x, mean, sq);
+            const float m = (float)mp[e % HW];
+            const float g = (-m * (x - yp[e])) / sigma2;
+            Y_next[idx] = (x + c1 * g) + c2 * z[j];
+        }
+    }
+}
+
 // PnP-ULA (restoration_algorithms.py:104-115)
 __global__ void pnpula_update_kernel(const float* X, const float* gp, const float* gd, float* Xo,
                                      float delta, float lambd, float brw, float cmin, float cmax, int B,
@@ -2143,6 +2188,7 @@ int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream) {
     a.n_tv = d->n_tv; a.seed = d->seed; a.chain0 = d->chain0; a.pingpong = 1;
     a.d_step = (long long*)s->d_step; a.step_offset = s->step_offset;
     a.fresh_dev = d->fresh; a.per_chain_norm = 1; a.norms = d->norms; a.arrive = d->arrive;
+    a.it0 = 0; a.last_chunk = 1; a.stopped = nullptr;
     a.advance_step = d->advance_step;
     a.stamps = (unsigned long long*)d->debug_stamps;
     a.n_inter = s->n_inter; a.nm = s->n_inter_mmse; a.coef = s->acc_coef;
@@ -2186,7 +2232,9 @@ int psgla_tv_prox(const PsglaTvProx* d, void* stream) {
     a.tau = d->tau; a.opt = d->one_plus_tau; a.inv_opt = (float)(1.0 / (double)d->one_plus_tau);
     a.sig_tv = d->sigma_tv; a.rho = d->rho; a.ths = d->ths; a.tol = d->tol;
     a.n_tv = d->n_tv; a.pingpong = 0;
-    a.fresh_host = d->fresh; a.per_chain_norm = 0; a.norms = d->norms; a.arrive = d->arrive;
+    a.fresh_host = d->fresh; a.per_chain_norm = d->per_chain ? 1 : 0; a.norms = d->norms; a.arrive = d->arrive;
+    if (d->it0 < 0) return fail(0, "psgla_tv_prox: it0 < 0");
+    a.it0 = d->it0; a.last_chunk = d->last_chunk ? 1 : 0; a.stopped = d->stopped;
     a.nm = -1;
     a.halo = d->n_tv;
     tv_tiling(a);
@@ -2295,14 +2343,20 @@ int psgla_relax_langevin_inpaint(const float* Y, const float* D, float* X, float
     if (!D || !y || !mask || !Y_next || !s || B <= 0 || C <= 0 || H <= 0 || W <= 0)
         return fail(0, "psgla_relax_langevin_inpaint: bad arguments");
     if (!alpha_is_one && !Y) return fail(0, "psgla_relax_langevin_inpaint: Y required when alpha != 1");
-    if (((long long)H * W) % 4 != 0) return fail(0, "psgla_relax_langevin_inpaint: H*W must be a multiple of 4");
     if (s->n_inter_mmse >= 0 && (!mean || !sq || !s->acc_coef))
         return fail(0, "psgla_relax_langevin_inpaint: accumulators missing");
     if ((long long)B * C > 65535) return fail(0, "psgla_relax_langevin_inpaint: more than 65535 planes in one launch");
-    hipLaunchKernelGGL(relax_langevin_inpaint_kernel, dim3(grid_chain((long long)H * W / 4 + 1, B * C), B * C),
-                       dim3(256), 0, (hipStream_t)stream, Y, D, X, alpha, (int)(alpha_is_one != 0), y,
-                       (long long)y_chain_stride, mask, (long long)mask_chain_stride, Y_next, B, C, H, W, sigma2, c1,
-                       c2, (unsigned long long)seed, chain0, mean, sq, make_acc(s));
+    if (((long long)H * W) % 4 == 0)
+        hipLaunchKernelGGL(relax_langevin_inpaint_kernel, dim3(grid_chain((long long)H * W / 4 + 1, B * C), B * C),
+                           dim3(256), 0, (hipStream_t)stream, Y, D, X, alpha, (int)(alpha_is_one != 0), y,
+                           (long long)y_chain_stride, mask, (long long)mask_chain_stride, Y_next, B, C, H, W, sigma2,
+                           c1, c2, (unsigned long long)seed, chain0, mean, sq, make_acc(s));
+    else
+        hipLaunchKernelGGL(relax_langevin_inpaint_any_kernel,
+                           dim3(grid_chain(((long long)C * H * W + 3) / 4, B), B), dim3(256), 0, (hipStream_t)stream,
+                           Y, D, X, alpha, (int)(alpha_is_one != 0), y, (long long)y_chain_stride, mask,
+                           (long long)mask_chain_stride, Y_next, B, C, H, W, sigma2, c1, c2,
+                           (unsigned long long)seed, chain0, mean, sq, make_acc(s));
     return launch_check("relax_langevin_inpaint");
 }
 

@@ -48,16 +48,23 @@ class TVDenoiser(torch.nn.Module):
     def needs_restart(self, shape) -> bool:
         return self.restart or self.x2 is None or tuple(self.x2.shape) != tuple(shape)
 
-    def forward(self, y, ths=None):
+    def forward(self, y, ths=None, per_chain: bool = False):
+        """deepinv's forward.  per_chain=True (this build's extension, used by psgla over a batch of
+        chains): the early stop is decided per chain -- each batch entry behaves as its own call --
+        instead of on the whole tensor as deepinv does.  Any n_it_max: above
+        PSGLA_TV_MAX_FUSED_IT the prox runs in chunks (hip_ops.tv_prox)."""
         if ths is None:
             raise TypeError("TVDenoiser.forward needs the threshold `ths` (the reference passes sigma)")
         y = y.contiguous()
         fresh = self.needs_restart(y.shape)
         k = self.constants()
-        if self._work is None or self._work.norms.shape[1] != max(k.n_it, 1) or self._work.norms.device != y.device:
-            self._work = K.TvWorkspace(1, k.n_it, y.device)
+        G = y.shape[0] if per_chain else 1
+        it = min(max(k.n_it, 1), K.N.TV_MAX_FUSED_IT)
+        if (self._work is None or self._work.norms.shape[0] < G or self._work.norms.shape[1] != it
+                or self._work.norms.device != y.device):
+            self._work = K.TvWorkspace(G, it, y.device)
         x2, u2 = K.tv_prox(y, float(ths), k, None if fresh else self.x2, None if fresh else self.u2,
-                           fresh=fresh, exact=self.exact, work=self._work)
+                           fresh=fresh, exact=self.exact, work=self._work, per_chain=per_chain)
         self.x2, self.u2 = x2, u2
         self.restart = False
         return x2
@@ -88,7 +95,10 @@ class DnCNN(torch.nn.Module):
         """relu(conv(h)).  On the GPU the bias add and the ReLU are one in-place HIP pass over the
         conv output (hip_ops.bias_act_: the same fp32 operations as PyTorch's bias add + ReLU, so the
         result is bit-identical) instead of two passes over a 64 x 64 x 256 x 256 activation."""
-        if h.is_cuda and conv.bias is not None and isinstance(self.nl_list[i], torch.nn.ReLU):
+        # the HIP pass is invisible to autograd: used only when no gradient can flow through it
+        no_grad = not torch.is_grad_enabled() or not (h.requires_grad or conv.weight.requires_grad
+                                                      or conv.bias is None or conv.bias.requires_grad)
+        if h.is_cuda and conv.bias is not None and isinstance(self.nl_list[i], torch.nn.ReLU) and no_grad:
             from . import hip_ops as K
             y = torch.nn.functional.conv2d(h, conv.weight, None, conv.stride, conv.padding)
             return K.bias_act_(y, conv.bias, relu=True)
@@ -163,17 +173,48 @@ class DRUNet(torch.nn.Module):
         if self.channels_last and x.is_cuda:
             self.to(memory_format=torch.channels_last)
             x = x.contiguous(memory_format=torch.channels_last)
-        return self._forward_padded(x).contiguous()
+        return self._forward_dispatch(x).contiguous()
 
-    def _forward_padded(self, x):
-        if x.size(2) % 8 == 0 and x.size(3) % 8 == 0:
-            return self.forward_unet(x)
-        # deepinv's test_pad: replicate-pad to a multiple of 8 (16 for images >= 32 px), crop back
+    def _forward_dispatch(self, x):
+        """deepinv 0.2.1 DRUNet.forward's size dispatch (KAIR utils_model): the U-Net itself when both
+        sides are multiples of 8 and > 31 (or in training mode); replicate padding to multiples of 16
+        (test_pad) when a side is < 32; otherwise four overlapping quadrants cut on a 64-pixel grid
+        (test_onesplit, refield 64), each run alone, stitched back."""
         h, w = x.size(2), x.size(3)
-        mod = 8 if (h < 32 or w < 32) else 16
-        ph, pw = (-h) % mod, (-w) % mod
-        y = self.forward_unet(torch.nn.functional.pad(x, (0, pw, 0, ph), mode="replicate"))
-        return y[..., :h, :w]
+        if self.training or (h % 8 == 0 and w % 8 == 0 and h > 31 and w > 31):
+            return self.forward_unet(x)
+        if h < 32 or w < 32:
+            return _test_pad(self.forward_unet, x, modulo=16)
+        return _test_onesplit(self.forward_unet, x, refield=64)
+
+
+def _test_pad(model, L, modulo: int = 16):
+    """KAIR utils_model.test_pad: replicate-pad bottom / right to multiples of `modulo`, crop back."""
+    h, w = L.size()[-2:]
+    pb = int(np.ceil(h / modulo) * modulo - h)
+    pr = int(np.ceil(w / modulo) * modulo - w)
+    E = model(torch.nn.functional.pad(L, (0, pr, 0, pb), mode="replicate"))
+    return E[..., :h, :w]
+
+
+def _test_onesplit(model, L, refield: int = 32, sf: int = 1):
+    """KAIR utils_model.test_onesplit: four corner crops of ((side // 2) // refield + 1) * refield
+    pixels per side, each through the model, the four quarters of the output taken from them."""
+    h, w = L.size()[-2:]
+    th = (h // 2 // refield + 1) * refield
+    tw = (w // 2 // refield + 1) * refield
+    top, bottom = slice(0, th), slice(h - th, h)
+    left, right = slice(0, tw), slice(w - tw, w)
+    Es = [model(L[..., top, left]), model(L[..., top, right]), model(L[..., bottom, left]),
+          model(L[..., bottom, right])]
+    b, c = Es[0].size()[:2]
+    E = torch.zeros(b, c, sf * h, sf * w, dtype=L.dtype, device=L.device)
+    h2, w2 = h // 2 * sf, w // 2 * sf
+    E[..., :h2, :w2] = Es[0][..., :h2, :w2]
+    E[..., :h2, w2:w * sf] = Es[1][..., :h2, (-w + w // 2) * sf:]
+    E[..., h2:h * sf, :w2] = Es[2][..., (-h + h // 2) * sf:, :w2]
+    E[..., h2:h * sf, w2:w * sf] = Es[3][..., (-h + h // 2) * sf:, (-w + w // 2) * sf:]
+    return E
 
 
 def drunet_flops_per_pixel(nc=(64, 128, 256, 512), nb: int = 4, c: int = 3) -> float:

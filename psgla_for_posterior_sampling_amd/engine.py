@@ -199,6 +199,12 @@ class FusedTvChains:
     def X(self) -> torch.Tensor:
         return self._view(self.x[self.steps_done & 1])
 
+    def input_state(self, step: int) -> torch.Tensor:
+        """X_step, the input of step `step` -- intact in its ping-pong buffer until step + 1 has run."""
+        if not (self.steps_done - 1 <= step <= self.steps_done):
+            raise ValueError("only the last step's input is still held")
+        return self._view(self.x[step & 1])
+
     @property
     def u2_state(self) -> torch.Tensor:
         return self._view(self.u2[self.steps_done & 1], u2=True)
@@ -264,6 +270,7 @@ class _GraphRunner:
 
     def capture(self, steps_per_graph: int):
         k = steps_per_graph + (steps_per_graph & 1)
+        self.graph_cur = self.cur          # the buffer parity the recorded pointers assume
         with torch.no_grad():
             self.graph = _capture(self._body, k, self.device)
         self.graph_steps = k
@@ -277,13 +284,19 @@ class _GraphRunner:
 
     def run(self, n: int | None = None, graph_steps: int = 0):
         n = self.n_iter - self.steps_done if n is None else n
-        # two eager steps first: the denoiser's kernels (MIOpen) pick their algorithms outside capture
-        warm = min(n, 2)
-        self.step(warm)
-        n -= warm
+        if self.steps_done < 2:
+            # two eager steps first: the denoiser's kernels (MIOpen) pick their algorithms outside capture
+            warm = min(n, 2 - self.steps_done)
+            self.step(warm)
+            n -= warm
         if graph_steps > 0 and n >= graph_steps:
             if self.graph is None or self.graph_steps != graph_steps + (graph_steps & 1):
                 self.capture(graph_steps)
+            if self.cur != self.graph_cur:
+                # an odd number of eager steps since the capture: one more, so the replayed pointers
+                # (recorded at parity graph_cur) see the buffers they were recorded with
+                self.step(1)
+                n -= 1
             reps = n // self.graph_steps
             self.replay(reps)
             n -= reps * self.graph_steps
@@ -310,8 +323,6 @@ class DenoiserChains(_GraphRunner):
         if not (self.inpaint or isinstance(data_grad, BlurFidelity)):
             raise TypeError("DenoiserChains needs an InpaintingFidelity or a BlurFidelity data term")
         B, C, H, W = init.shape
-        if self.inpaint and (H * W) % 4:
-            raise ValueError("the fused inpainting pass needs H*W % 4 == 0")
         self.device = init.device
         self.shape = (B, C, H, W)
         self.fid = data_grad
@@ -324,6 +335,8 @@ class DenoiserChains(_GraphRunner):
         X0 = init.contiguous().float()
         self.Y = [torch.empty_like(X0), torch.empty_like(X0)]
         self.X = None if self.inpaint else torch.empty_like(X0)
+        self._keep = False          # step_keep_state(): materialise X_{i+1} (inpainting writes it only then)
+        self._Xsnap = None
         self.mean = torch.zeros_like(X0)
         self.sq = torch.zeros_like(X0)
         self.sched = K.Schedule(self.shape, n_iter, n_inter, n_inter_mmse, self.device)
@@ -345,14 +358,39 @@ class DenoiserChains(_GraphRunner):
         D = self.denoiser.forward(Yc, self.sig).contiguous().float()
         f = self.fid
         if self.inpaint:
+            xo = None
+            if self._keep:
+                if self._Xsnap is None:
+                    self._Xsnap = torch.empty_like(Yc)
+                xo = self._Xsnap
             K.relax_langevin_inpaint(Yc, D, self.alpha, f.y, f.mask_u8, f.sigma2, self.c1, self.c2, self.seed,
-                                     self.chain0, self.mean, self.sq, self.sched, 0, Yn, use_device_step=True)
+                                     self.chain0, self.mean, self.sq, self.sched, 0, Yn, X_out=xo,
+                                     use_device_step=True)
         else:
             K.relax_accumulate(Yc, D, self.X, self.alpha, self.mean, self.sq, self.sched, 0, use_device_step=True)
             K.blur_langevin(self.X, f.y.contiguous(), f.taps_conv, f.taps_corr, f.l, f.sigma2, self.c1, self.c2,
                             self.seed, self.chain0, 1, out=Yn, exact=f.exact, d_step=self.sched.d_step)
         K.advance_step(self.sched.d_step)
         self.cur ^= 1
+
+    def step_keep_state(self):
+        """One eager step i that also keeps what save_images_online shows (restoration_algorithms.py:246-253):
+        X_{i+1} (``X_state``) and the step's Langevin proposal Y_i (``Y_prev``)."""
+        self._keep = True
+        try:
+            self.step(1)
+        finally:
+            self._keep = False
+
+    @property
+    def X_state(self) -> torch.Tensor:
+        """X after the last step run by step_keep_state() (inpainting) / the last step (deblurring)."""
+        return self._Xsnap if self.inpaint else self.X
+
+    @property
+    def Y_prev(self) -> torch.Tensor:
+        """Y_i of the last step run (the buffer the next step overwrites)."""
+        return self.Y[1 - self.cur]
 
 
 class UlaChains(_GraphRunner):

@@ -246,16 +246,9 @@ class TvConstants:
         self.n_it = int(n_it_max)
 
 
-def tv_prox(y: torch.Tensor, ths: float, k: TvConstants, x2_in=None, u2_in=None, fresh: bool = True,
-            exact: bool = False, x2_out=None, u2_out=None, work=None):
-    """One TVDenoiser.forward on the GPU; returns (x2_out, u2_out)."""
+def _tv_prox_launch(y, ths, k: TvConstants, n_it: int, x2_in, u2_in, fresh: bool, exact: bool, x2_out, u2_out,
+                    work, per_chain: bool, it0: int, last: bool, stopped):
     B, C, H, W = y.shape
-    if x2_out is None:
-        x2_out = torch.empty_like(y)
-    if u2_out is None:
-        u2_out = torch.empty(y.shape + (2,), dtype=torch.float32, device=y.device)
-    if work is None:
-        work = TvWorkspace(1, k.n_it, y.device)
     d = N.PsglaTvProx()
     d.B, d.C, d.H, d.W = B, C, H, W
     d.y = _ptr(y, name="y")
@@ -266,12 +259,65 @@ def tv_prox(y: torch.Tensor, ths: float, k: TvConstants, x2_in=None, u2_in=None,
     d.tau, d.one_plus_tau, d.sigma_tv, d.rho = k.tau, k.one_plus_tau, k.sigma_tv, k.rho
     d.ths = float(np.float32(ths))
     d.tol = k.tol
-    d.n_tv = k.n_it
+    d.n_tv = n_it
     d.exact = int(bool(exact))
     d.fresh = int(bool(fresh))
     d.norms = work.norms.data_ptr()
     d.arrive = work.arrive.data_ptr()
+    d.per_chain = int(bool(per_chain))
+    d.it0 = int(it0)
+    d.last_chunk = int(bool(last))
+    d.stopped = stopped.data_ptr() if stopped is not None else None
     N.check(N.lib().psgla_tv_prox(ctypes.byref(d), _stream()), "psgla_tv_prox")
+
+
+def tv_prox(y: torch.Tensor, ths: float, k: TvConstants, x2_in=None, u2_in=None, fresh: bool = True,
+            exact: bool = False, x2_out=None, u2_out=None, work=None, per_chain: bool = False):
+    """One TVDenoiser.forward on the GPU; returns (x2_out, u2_out).
+
+    per_chain: deepinv's early stop on each chain of the batch (B independent reference runs) instead
+    of on the whole tensor.  n_it_max above N.TV_MAX_FUSED_IT runs as chunks of at most that many
+    inner iterations (psgla_tv_prox's it0 / last_chunk / stopped): after each chunk but the last the
+    host reads which groups stopped inside it and keeps their result (one host sync per chunk)."""
+    B, C, H, W = y.shape
+    G = B if per_chain else 1
+    if x2_out is None:
+        x2_out = torch.empty_like(y)
+    if u2_out is None:
+        u2_out = torch.empty(y.shape + (2,), dtype=torch.float32, device=y.device)
+    n = k.n_it
+    cmax = N.TV_MAX_FUSED_IT
+    if work is None or work.norms.shape[0] < G or work.norms.shape[1] < min(max(n, 1), cmax):
+        work = TvWorkspace(G, min(max(n, 1), cmax), y.device)
+    if n <= cmax:
+        _tv_prox_launch(y, ths, k, n, x2_in, u2_in, fresh, exact, x2_out, u2_out, work, per_chain, 0, True, None)
+        return x2_out, u2_out
+    # chunked: ping-pong between two scratch pairs; a group's result is final at its stop
+    bufs = [(torch.empty_like(y), torch.empty_like(u2_out)) for _ in range(2)]
+    stopped = torch.zeros(G, dtype=torch.int32, device=y.device)
+    done = np.zeros(G, dtype=bool)
+    cur_x2, cur_u2, cur_fresh = x2_in, u2_in, fresh
+    nch = (n + cmax - 1) // cmax
+    rows = (lambda g: slice(g, g + 1)) if per_chain else (lambda g: slice(None))
+    for c in range(nch):
+        it0 = c * cmax
+        last = c == nch - 1
+        ox2, ou2 = bufs[c & 1]
+        _tv_prox_launch(y, ths, k, min(cmax, n - it0), cur_x2, cur_u2, cur_fresh, exact, ox2, ou2, work, per_chain,
+                        it0, last, None if last else stopped)
+        cur_x2, cur_u2, cur_fresh = ox2, ou2, False
+        if last:
+            break
+        st = stopped.cpu().numpy()
+        for g in np.nonzero((st > 0) & ~done)[0]:
+            x2_out[rows(g)].copy_(ox2[rows(g)])
+            u2_out[rows(g)].copy_(ou2[rows(g)])
+            done[g] = True
+        if done.all():
+            return x2_out, u2_out
+    for g in np.nonzero(~done)[0]:
+        x2_out[rows(g)].copy_(cur_x2[rows(g)])
+        u2_out[rows(g)].copy_(cur_u2[rows(g)])
     return x2_out, u2_out
 
 

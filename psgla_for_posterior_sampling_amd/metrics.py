@@ -4,7 +4,9 @@ PSNR and SSIM restate scikit-image 0.24's ``peak_signal_noise_ratio`` and
 ``structural_similarity`` with the arguments the reference passes (data_range=1, default
 7x7 uniform window, sample covariance, K1=0.01, K2=0.03, mean over channel_axis=2).
 scikit-image is not installed in this image, so the restatement is *parity unpinned*: it is
-checked against closed-form cases in tests/test_metrics.py, not against skimage outputs.
+checked against closed-form cases and a direct evaluation in tests/test_metrics_cli.py, not
+against skimage outputs; everything around PSNR / SSIM in ``analyse_run`` is pinned to the reference
+sampling_images.py:371-442 executed on fixture outputs (tests/golden/postproc_inpaint_tv.npz).
 """
 from __future__ import annotations
 

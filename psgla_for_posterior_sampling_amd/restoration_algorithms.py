@@ -61,19 +61,44 @@ def _lists(sched: K.Schedule, steps_done: int):
     return Xlist, M, M2
 
 
-def _save_online(path, name, i, X, Y, sched, steps_done, extra):
-    import matplotlib
-    matplotlib.use("Agg")
-    import matplotlib.pyplot as plt
-    xn = np.transpose(X.detach().cpu().numpy()[0], (1, 2, 0))
-    plt.imsave(path + "/x_" + str(i) + ".png", np.clip(xn, 0, 1), cmap=None)
-    if Y is not None:
-        yn = np.transpose(Y.detach().cpu().numpy()[0], (1, 2, 0))
-        plt.imsave(path + "/y_" + str(i) + ".png", np.clip(yn, 0, 1), cmap=None)
-    Xl, M, M2 = _lists(sched, steps_done)
-    d = {"Samples": Xl, "Mmse": M, "Mmse2": M2}
-    d.update(extra)
-    torch.save(d, path + "/" + name + "_sampling.pth")
+class _Snapshots:
+    """``save_images_online`` (restoration_algorithms.py:246-253 + :273-283 for psgla, :124-127 +
+    :146-158 for pnpula): after every step i with i % K == 0 (K = int(n_iter / 10)), x_i.png (and
+    y_i.png for psgla) of chain 0 -- the reference runs one chain, ``X.numpy()[0]`` --, then
+    ``torch.save`` of the dict {'Samples', 'Mmse', 'Mmse2', <run parameters>} with the lists as they
+    stand after step i.  The list tensors are saved as copies: views would serialise the whole
+    sample / block store they live in."""
+
+    def __init__(self, path, name, extra):
+        self.path, self.name, self.extra = path, name, extra
+
+    @staticmethod
+    def _png(fname, t):
+        import matplotlib
+        matplotlib.use("Agg")
+        import matplotlib.pyplot as plt
+        a = np.transpose(t.detach().cpu().numpy()[0, :, :, :], (1, 2, 0))
+        plt.imsave(fname, np.clip(a, 0, 1), cmap=None)
+
+    def save(self, i, X, Y, lists):
+        self._png(self.path + "/x_" + str(i) + ".png", X)
+        if Y is not None:
+            self._png(self.path + "/y_" + str(i) + ".png", Y)
+        Xl, M, M2 = lists
+        d = {"Samples": [t.clone() for t in Xl], "Mmse": [t.clone() for t in M], "Mmse2": [t.clone() for t in M2]}
+        d.update(self.extra)
+        torch.save(d, self.path + "/" + self.name + "_sampling.pth")
+
+
+def _run_with_snapshots(run, n_iter: int, Kfreq: int, snap):
+    """Run n_iter steps through ``run(n)`` and call ``snap(i)`` right after every step i with
+    i % Kfreq == 0 (the reference's cadence, restoration_algorithms.py:246, :273)."""
+    done = 0
+    for i in range(0, n_iter, Kfreq):
+        run(i + 1 - done)
+        done = i + 1
+        snap(i)
+    run(n_iter - done)
 
 
 def psgla(init, data_grad, denoiser, alpha, lambd, sig_float=0.0055, delta=4e-5, n_iter=5000, n_inter=1000,
@@ -103,8 +128,12 @@ def psgla(init, data_grad, denoiser, alpha, lambd, sig_float=0.0055, delta=4e-5,
     if graph_steps is None:
         graph_steps = DEFAULT_GRAPH_STEPS
 
+    snaps = None
+    if save_images_online:
+        snaps = _Snapshots(path, name, {"n_iter": n_iter, "lambda": lambd, "delta": delta_t.to(dev)})
+
     fused = (isinstance(data_grad, InpaintingFidelity) and isinstance(denoiser, TVDenoiser)
-             and denoiser.n_it_max <= K.N.TV_MAX_FUSED_IT and not save_images_online)
+             and denoiser.n_it_max <= K.N.TV_MAX_FUSED_IT)
     if fused:
         if exact is None:
             exact = denoiser.exact
@@ -113,21 +142,51 @@ def psgla(init, data_grad, denoiser, alpha, lambd, sig_float=0.0055, delta=4e-5,
                             alpha=alpha_f, ths=float(np.float32(sig_noised)), tv=denoiser.constants(), seed=seed,
                             n_iter=n_iter, n_inter=n_inter, n_inter_mmse=n_inter_mmse, chain0=chain0,
                             exact=exact, tv_x2=denoiser.x2 if warm else None, tv_u2=denoiser.u2 if warm else None)
-        eng.run(n_iter, graph_steps=graph_steps if n_iter >= 2 * graph_steps else 0)
+
+        def run_fused(n):
+            eng.run(n, graph_steps=graph_steps if n >= 2 * graph_steps else 0)
+
+        if snaps is None:
+            run_fused(n_iter)
+        else:
+            def snap(i):
+                # Y_i of the step just run, recomputed from its input X_i (still in the ping-pong buffer)
+                Xi = eng.input_state(i).contiguous()
+                Yi = K.langevin_update(Xi, K.inpaint_grad(Xi, data_grad.y, data_grad.mask_u8, data_grad.sigma2),
+                                       c1, c2, seed, chain0, i)
+                snaps.save(i, eng.X, Yi, eng.lists())
+            _run_with_snapshots(run_fused, n_iter, Kfreq, snap)
         denoiser.x2 = eng.x2_state.contiguous().clone()
         denoiser.u2 = eng.u2_state.contiguous().clone()
         denoiser.restart = False
         return eng.lists()
 
     typed = isinstance(data_grad, (InpaintingFidelity, BlurFidelity))
-    if (typed and isinstance(denoiser, torch.nn.Module) and not isinstance(denoiser, TVDenoiser)
-            and not save_images_online and not (isinstance(data_grad, InpaintingFidelity)
-                                                and (shape[2] * shape[3]) % 4)):
+    if typed and isinstance(denoiser, torch.nn.Module) and not isinstance(denoiser, TVDenoiser):
         sig_den = torch.tensor(sig_noised).to(dev).to(torch.float32)
         eng = DenoiserChains(X0, data_grad, denoiser, sig_den, alpha=alpha_f, c1=c1, c2=c2, seed=seed,
                              n_iter=n_iter, n_inter=n_inter, n_inter_mmse=n_inter_mmse, chain0=chain0)
         capturable = isinstance(denoiser, (DnCNN, DRUNet)) or getattr(denoiser, "capturable", False)
-        eng.run(n_iter, graph_steps=graph_steps if (capturable and n_iter >= 2 * graph_steps) else 0)
+
+        def run_dnn(n):
+            eng.run(n, graph_steps=graph_steps if (capturable and n >= 2 * graph_steps) else 0)
+
+        if snaps is None:
+            run_dnn(n_iter)
+        else:
+            def run_until_snapshot(n):
+                run_dnn(n - 1)
+                if n > 0:
+                    eng.step_keep_state()       # the snapshot step: X_{i+1} materialised, Y_i kept
+
+            def snap(i):
+                snaps.save(i, eng.X_state, eng.Y_prev, _lists(eng.sched, eng.steps_done))
+            done = 0
+            for i in range(0, n_iter, Kfreq):
+                run_until_snapshot(i + 1 - done)
+                done = i + 1
+                snap(i)
+            run_dnn(n_iter - done)
         return _lists(eng.sched, eng.steps_done)
 
     # ---- generic path: opaque closures, HIP noise / update / relaxation / accumulators ----
@@ -138,6 +197,7 @@ def psgla(init, data_grad, denoiser, alpha, lambd, sig_float=0.0055, delta=4e-5,
     mean = torch.zeros_like(X)
     sq = torch.zeros_like(X)
     sig_den = torch.tensor(sig_noised).to(dev).to(torch.float32)
+    tv_batch = isinstance(denoiser, TVDenoiser)
     with torch.no_grad():
         blur = isinstance(data_grad, BlurFidelity)
         for i in range(n_iter):
@@ -147,12 +207,12 @@ def psgla(init, data_grad, denoiser, alpha, lambd, sig_float=0.0055, delta=4e-5,
             else:
                 g = data_grad(X)
                 K.langevin_update(X, g.contiguous().float(), c1, c2, seed, chain0, i, out=Y)
-            D = denoiser.forward(Y, sig_den)
+            # a TV prox over B chains: deepinv's early stop per chain (each chain is one reference run)
+            D = denoiser.forward(Y, sig_den, per_chain=True) if tv_batch else denoiser.forward(Y, sig_den)
             K.relax_accumulate(Y, D.contiguous(), Xn, alpha_f, mean, sq, sched, i)
             X, Xn = Xn, X
-            if i % Kfreq == 0 and save_images_online:
-                _save_online(path, name, i, X, Y, sched, i + 1,
-                             {"n_iter": n_iter, "lambda": lambd, "delta": delta_t.to(dev)})
+            if i % Kfreq == 0 and snaps is not None:
+                snaps.save(i, X, Y, _lists(sched, i + 1))
     return _lists(sched, n_iter)
 
 
@@ -175,14 +235,25 @@ def pnpula(init, data_grad, prior_grad, delta, lambd, n_iter=5000, n_inter=1000,
     lam = float(torch.as_tensor(lambd).detach().cpu().to(torch.float32).item())
     if graph_steps is None:
         graph_steps = DEFAULT_GRAPH_STEPS
-    if (isinstance(prior_grad, DenoiserPrior) and isinstance(data_grad, (InpaintingFidelity, BlurFidelity))
-            and not save_images_online):
+    snaps = None
+    if save_images_online:
+        snaps = _Snapshots(path, name, {"n_iter": n_iter, "c_min": c_min, "c_max": c_max, "lambda": lambd,
+                                        "delta": delta})
+    if isinstance(prior_grad, DenoiserPrior) and isinstance(data_grad, (InpaintingFidelity, BlurFidelity)):
         eng = UlaChains(X, data_grad, prior_grad, delta=d, lambd=lam, brw=brw, c_min=float(c_min),
                         c_max=float(c_max), seed=int(seed), n_iter=n_iter, n_inter=n_inter,
                         n_inter_mmse=n_inter_mmse, chain0=chain0)
         capturable = isinstance(prior_grad.denoiser, (DnCNN, DRUNet)) or getattr(prior_grad.denoiser, "capturable",
                                                                                 False)
-        eng.run(n_iter, graph_steps=graph_steps if (capturable and n_iter >= 2 * graph_steps) else 0)
+
+        def run_ula(n):
+            eng.run(n, graph_steps=graph_steps if (capturable and n >= 2 * graph_steps) else 0)
+
+        if snaps is None:
+            run_ula(n_iter)
+        else:
+            _run_with_snapshots(run_ula, n_iter, Kfreq,
+                                lambda i: snaps.save(i, eng.state, None, _lists(eng.sched, eng.steps_done)))
         return _lists(eng.sched, eng.steps_done)
     sched = K.Schedule(shape, n_iter, n_inter, n_inter_mmse, dev)
     Xn = torch.empty_like(X)
@@ -195,7 +266,6 @@ def pnpula(init, data_grad, prior_grad, delta, lambd, n_iter=5000, n_inter=1000,
             K.pnpula_update(X, gp, gd, Xn, d, lam, brw, float(c_min), float(c_max), mean, sq, sched, i,
                             int(seed), chain0)
             X, Xn = Xn, X
-            if i % Kfreq == 0 and save_images_online:
-                _save_online(path, name, i, X, None, sched, i + 1,
-                             {"n_iter": n_iter, "c_min": c_min, "c_max": c_max, "lambda": lambd, "delta": delta})
+            if i % Kfreq == 0 and snaps is not None:
+                snaps.save(i, X, None, _lists(sched, i + 1))
     return _lists(sched, n_iter)

@@ -267,6 +267,41 @@ def main():
         json.dump(params, f, indent=1, sort_keys=True)
     print("wrote params.json")
 
+    make_postproc()
+
+
+def reference_postproc(im, samples_t, mmse_t, mmse2_t, y_t, init_torch, grayscale=False):
+    """Execute the reference's per-image post-processing, sampling_images.py:371-442, on given
+    chain outputs.  PSNR / ssim are bound to this build's metrics.psnr / metrics.ssim (scikit-image
+    is not installed): the fixture pins everything AROUND them -- sample / block conversion, the
+    running-MMSE curve (range(1, n)), MMSE, std, diff, min / max -- to the reference's own code."""
+    from psgla_for_posterior_sampling_amd import metrics
+    pars = types.SimpleNamespace(grayscale=grayscale)
+    ns = dict(np=np, torch=torch, pars=pars, im=im, Samples_t=samples_t, Mmse_t=mmse_t, Mmse2_t=mmse2_t,
+              y_t=y_t, init_torch=init_torch, PSNR=metrics.psnr, ssim=metrics.ssim)
+    exec(compile(reference_source("sampling_images.py", 371, 442), "sampling_images.py:371", "exec"), ns)
+    return ns
+
+
+def make_postproc():
+    """(7) sampling_images.py:371-442 on the chain outputs of fixture (2) (psgla + TV): the
+    reference's result-dict values, for metrics.analyse_run (tests/test_metrics_cli.py)."""
+    z = np.load(os.path.join(HERE, "psgla_inpaint_tv.npz"))
+    im = np.float32(np.transpose(z["x"][0], (1, 2, 0)))
+    samples_t = [torch.from_numpy(s) for s in z["samples"]]
+    mmse_t = [torch.from_numpy(s) for s in z["blocks"]]
+    mmse2_t = [torch.from_numpy(s) for s in z["blocks2"]]
+    ns = reference_postproc(im, samples_t, mmse_t, mmse2_t, torch.from_numpy(z["y"]), torch.from_numpy(z["init"]))
+    save("postproc_inpaint_tv", PSNR_sample=np.array(ns["Psnr_sample"], np.float64),
+         SIM_sample=np.array(ns["SIM_sample"], np.float64), PSNR_mmse=np.array(ns["PSNR_list"], np.float64),
+         SIM_list=np.array(ns["SIM_list"], np.float64), Min_sample=np.array(ns["Min_sample"]),
+         Max_sample=np.array(ns["Max_sample"]), observation=ns["y"], init=ns["init"], PSNR_y=ns["psb"],
+         SIM_y=ns["ssb"], MMSE=ns["xmmse"], PSNR_MMSE=ns["pmmse"], SIM_MMSE=ns["smmse"], std=ns["std"],
+         diff=ns["diff"], mean_list=ns["mean_list"])
+
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["postproc"]:
+        make_postproc()
+    else:
+        main()

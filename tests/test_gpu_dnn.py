@@ -197,3 +197,160 @@ def test_dncnn_fused_epilogue_equals_torch_layers():
             h = m.nl_list[i + 1](m.conv_list[i](h))
         ref = (m.out_conv(h) + xc).contiguous()
     assert rel(out.cpu().numpy(), ref.cpu().numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("alpha", [1.0, 0.6])
+def test_relax_langevin_inpaint_odd_plane_equals_unfused(alpha):
+    """H*W % 4 != 0 (set1c / CBSD68 are 481 x 321): the chain-quad variant of the fused pass equals
+    relax_accumulate + inpaint_grad + langevin_update bit for bit."""
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    B, C, H, W = 2, 3, 37, 45
+    dg, _ = problem(B=B, H=H, W=W)
+    g = torch.Generator(device=DEV).manual_seed(6)
+    c1, c2, seed = 0.8 * (1 / 255.0) ** 2, 0.011, 9
+    sched_a = K.Schedule((B, C, H, W), 8, 3, 2, DEV)
+    sched_b = K.Schedule((B, C, H, W), 8, 3, 2, DEV)
+    ma, qa = torch.zeros(B, C, H, W, device=DEV), torch.zeros(B, C, H, W, device=DEV)
+    mb, qb = ma.clone(), qa.clone()
+    for i in range(8):
+        Y = torch.rand((B, C, H, W), generator=g, device=DEV)
+        D = torch.rand((B, C, H, W), generator=g, device=DEV)
+        Yn_a, Xa = torch.empty_like(Y), torch.empty_like(Y)
+        K.relax_langevin_inpaint(Y, D, alpha, dg.y, dg.mask_u8, dg.sigma2, c1, c2, seed, 2, ma, qa, sched_a, i, Yn_a,
+                                 X_out=Xa)
+        Xb = K.relax_accumulate(Y, D, torch.empty_like(Y), alpha, mb, qb, sched_b, i)
+        Yn_b = K.langevin_update(Xb, K.inpaint_grad(Xb, dg.y, dg.mask_u8, dg.sigma2), c1, c2, seed, 2, i + 1)
+        torch.cuda.synchronize()
+        assert torch.equal(Xa, Xb) and torch.equal(Yn_a, Yn_b)
+        assert torch.equal(ma, mb) and torch.equal(qa, qb)
+    assert torch.equal(sched_a.samples, sched_b.samples) and torch.equal(sched_a.blocks, sched_b.blocks)
+
+
+def test_denoiser_chains_odd_plane_graph_equals_step_loop():
+    """Config 3 on a 481 x 321-like plane (here 37 x 45: H*W odd): DenoiserChains runs hipGraph-captured
+    and equals the generic step-by-step loop bit for bit."""
+    from psgla_for_posterior_sampling_amd import restoration_algorithms as RA
+    dg, init = problem(B=2, H=37, W=45)
+    den = small_dncnn().to(DEV)
+    kw = dict(sig_float=2 / 255.0, delta=6.1515e-5, n_iter=30, n_inter=3, n_inter_mmse=4, seed=5)
+    a = RA.psgla(init, dg, den, torch.tensor(1.0), torch.tensor(5.0), graph_steps=6, **kw)
+    b = RA.psgla(init, lambda x: dg(x), den, torch.tensor(1.0), torch.tensor(5.0), **kw)
+    for la, lb in zip(a, b):
+        assert len(la) == len(lb) > 0
+        for u, v in zip(la, lb):
+            assert torch.equal(u, v)
+
+
+def _check_snapshots(path, name, n_iter, lists, extra_keys, with_y, B):
+    import os
+    K_ = n_iter // 10
+    files = sorted(os.listdir(path))
+    xs = sorted(f for f in files if f.startswith("x_"))
+    assert xs == sorted(f"x_{i}.png" for i in range(0, n_iter, K_))
+    ys = sorted(f for f in files if f.startswith("y_"))
+    assert ys == (sorted(f"y_{i}.png" for i in range(0, n_iter, K_)) if with_y else [])
+    d = torch.load(os.path.join(path, name + "_sampling.pth"), weights_only=True)   # our own output file
+    assert set(d) == {"Samples", "Mmse", "Mmse2", "n_iter"} | set(extra_keys)
+    # the last snapshot was taken after step i_last: the lists as they stood then
+    i_last = ((n_iter - 1) // K_) * K_
+    for key, full in zip(("Samples", "Mmse", "Mmse2"), lists):
+        assert 0 < len(d[key]) <= len(full)
+        for u, v in zip(d[key], full):
+            assert torch.equal(u, v)
+    return i_last
+
+
+@pytest.mark.parametrize("den_kind", ["tv", "dncnn", "ula"])
+def test_save_images_online_keeps_the_fast_path(tmp_path, den_kind):
+    """save_images_online (restoration_algorithms.py:246-253, :273-283; :124-127, :146-158) on the
+    engines themselves: the returned lists equal the run without snapshots bit for bit, x_i / y_i PNGs
+    exist for exactly i % (n_iter / 10) == 0, and the saved dict has the reference's keys with the lists
+    as they stood at the last snapshot."""
+    from psgla_for_posterior_sampling_amd import restoration_algorithms as RA
+    from psgla_for_posterior_sampling_amd.denoisers import DenoiserPrior, TVDenoiser
+    B, n = 3, 40
+    dg, init = problem(B=B, H=24, W=40)
+    path = str(tmp_path)
+    if den_kind == "ula":
+        den = small_dncnn().to(DEV)
+        prior = DenoiserPrior(den, 5 / 255.0 / 255.0, torch.tensor(1.0, device=DEV),
+                              torch.tensor((5 / 255.0 / 255.0) ** 2, device=DEV))
+        kw = dict(n_iter=n, n_inter=3, n_inter_mmse=4, seed=4, graph_steps=4)
+        delta = torch.tensor(1e-6, device=DEV)
+        a = RA.pnpula(init, dg, prior, delta, torch.tensor(1e-5), **kw)
+        b = RA.pnpula(init, dg, prior, delta, torch.tensor(1e-5), path=path, save_images_online=True, name="nm",
+                      **kw)
+        extra, with_y = ("c_min", "c_max", "lambda", "delta"), False
+    else:
+        if den_kind == "tv":
+            s, lam, mk = 10 / 255.0, 10.0, (lambda: TVDenoiser(n_it_max=10, exact=True))
+        else:
+            s, lam, mk = 2 / 255.0, 5.0, (lambda: small_dncnn().to(DEV))
+        kw = dict(sig_float=s, delta=s ** 2, n_iter=n, n_inter=3, n_inter_mmse=4, seed=4, graph_steps=4)
+        a = RA.psgla(init, dg, mk(), torch.tensor(1.0), torch.tensor(lam), **kw)
+        b = RA.psgla(init, dg, mk(), torch.tensor(1.0), torch.tensor(lam), path=path, save_images_online=True,
+                     name="nm", **kw)
+        assert torch.isfinite(torch.stack(a[1])).all()
+        extra, with_y = ("lambda", "delta"), True
+    for la, lb in zip(a, b):
+        assert len(la) == len(lb) > 0
+        for u, v in zip(la, lb):
+            assert torch.equal(u, v)
+    i_last = _check_snapshots(path, "nm", n, b, extra, with_y, B)
+    d = torch.load(path + "/nm_sampling.pth", weights_only=True)
+    assert len(d["Samples"]) == i_last // 3 + 1          # samples at i % n_inter == 0, i <= i_last
+    assert len(d["Mmse"]) == (i_last + 1) // 5           # blocks of n_inter_mmse + 1 steps completed
+    assert d["n_iter"] == n
+
+
+def test_tv_prox_long_n_it_chunked_vs_oracle():
+    """n_it_max = 30 > PSGLA_TV_MAX_FUSED_IT: the prox runs as two chunks (24 + 6 inner iterations) and is
+    bit-identical to deepinv's loop (oracle), cold and warm-started, with and without an early stop."""
+    from psgla_for_posterior_sampling_amd.denoisers import TVDenoiser
+    g = torch.Generator().manual_seed(3)
+    y = torch.rand((1, 3, 20, 28), generator=g)
+    for tol in (1e-5, 2e-3):                    # 2e-3: deepinv stops inside the first chunk or the second
+        ref = orc.TVDenoiser(n_it_max=30, tol=tol)
+        den = TVDenoiser(n_it_max=30, tol=tol, exact=True)
+        for call in range(3):
+            yy = y + 0.02 * call
+            r = ref.forward(yy, 0.05)
+            o = den.forward(yy.to(DEV), 0.05)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(o.cpu().numpy(), r.numpy(), err_msg=f"tol {tol} call {call}")
+            np.testing.assert_array_equal(den.u2.cpu().numpy(), ref.u2.numpy())
+
+
+def test_tv_prox_per_chain_early_stop_equals_single_chain_calls():
+    """per_chain=True on a batch of chains == one call per chain (deepinv's whole-tensor norm per chain),
+    including one chain that early-stops while the others do not."""
+    from psgla_for_posterior_sampling_amd.denoisers import TVDenoiser
+    g = torch.Generator().manual_seed(4)
+    y = torch.rand((3, 3, 18, 26), generator=g)
+    y[1] = 0.5 + 0.001 * y[1]                 # nearly flat: converges (stops) within a few iterations
+    for n_it in (10, 30):
+        den = TVDenoiser(n_it_max=n_it, tol=1e-3, exact=True)
+        singles = [TVDenoiser(n_it_max=n_it, tol=1e-3, exact=True) for _ in range(3)]
+        for call in range(2):
+            yy = (y + 0.01 * call).to(DEV)
+            o = den.forward(yy, 0.05, per_chain=True)
+            for b in range(3):
+                ob = singles[b].forward(yy[b:b + 1].contiguous(), 0.05)
+                assert torch.equal(o[b:b + 1], ob), (n_it, call, b)
+                assert torch.equal(den.u2[b:b + 1], singles[b].u2)
+
+
+def test_generic_tv_path_batch_equals_fused():
+    """A B > 1 TV run through the generic loop (opaque data_grad closure) equals the fused kernel's run:
+    per-chain early stop on both paths (restoration_algorithms.py:238 called once per chain by the
+    reference)."""
+    from psgla_for_posterior_sampling_amd import restoration_algorithms as RA
+    from psgla_for_posterior_sampling_amd.denoisers import TVDenoiser
+    dg, init = problem(B=3, H=24, W=40)
+    kw = dict(sig_float=10 / 255.0, delta=(10 / 255.0) ** 2, n_iter=20, n_inter=3, n_inter_mmse=4, seed=2)
+    a = RA.psgla(init, dg, TVDenoiser(n_it_max=10, exact=True), torch.tensor(1.0), torch.tensor(10.0), **kw)
+    b = RA.psgla(init, lambda x: dg(x), TVDenoiser(n_it_max=10, exact=True), torch.tensor(1.0), torch.tensor(10.0),
+                 **kw)
+    for la, lb in zip(a, b):
+        for u, v in zip(la, lb):
+            assert torch.equal(u, v)

@@ -70,6 +70,34 @@ def test_analyse_run_record_keys_and_values():
     assert np.all(rec["std"] >= 0)
 
 
+def _postproc_inputs(golden_dir):
+    import torch
+    z = np.load(os.path.join(golden_dir, "psgla_inpaint_tv.npz"))
+    im = np.float32(np.transpose(z["x"][0], (1, 2, 0)))
+    return (im, [torch.from_numpy(s) for s in z["samples"]], [torch.from_numpy(s) for s in z["blocks"]],
+            [torch.from_numpy(s) for s in z["blocks2"]], torch.from_numpy(z["y"]), torch.from_numpy(z["init"]))
+
+
+def test_analyse_run_matches_reference_postprocessing(golden_dir):
+    """metrics.analyse_run against sampling_images.py:371-442 executed on the psgla+TV fixture's chain
+    outputs (tests/golden/make_golden.py make_postproc, PSNR / ssim bound to metrics.*): every
+    result-dict value is identical -- the curve over range(1, n), MMSE, std, diff, min / max, and the
+    float32 / float64 types the reference's numpy expressions produce.  SSIM's own arithmetic stays
+    parity unpinned (skimage absent)."""
+    ref = np.load(os.path.join(golden_dir, "postproc_inpaint_tv.npz"))
+    im, samples, blocks, blocks2, y, init = _postproc_inputs(golden_dir)
+    rec, ex = metrics.analyse_run(im, samples, blocks, blocks2, y, init)
+    for k in ("PSNR_sample", "SIM_sample", "PSNR_mmse", "SIM_list"):
+        np.testing.assert_array_equal(np.array(rec[k], np.float64), ref[k], err_msg=k)
+    for k in ("PSNR_y", "SIM_y", "PSNR_MMSE", "SIM_MMSE"):
+        assert rec[k] == float(ref[k]), k
+    for k in ("observation", "init", "MMSE", "std", "diff"):
+        assert rec[k].dtype == ref[k].dtype, k
+        np.testing.assert_array_equal(rec[k], ref[k], err_msg=k)
+    np.testing.assert_array_equal(np.array(ex["Min_sample"]), ref["Min_sample"])
+    np.testing.assert_array_equal(np.array(ex["Max_sample"]), ref["Max_sample"])
+
+
 def test_parameters_follow_flag_presence():
     p = SI.build_parser()
     argv = ["--alg", "psgla", "--den", "TV"]
