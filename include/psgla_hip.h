@@ -76,6 +76,9 @@ typedef struct PsglaSchedule {
  *     H >= 2, every width with column segments): ONE launch per step; its last
  *     workgroup to finish evaluates the early stop, re-streams stopped chains and
  *     advances the step (no second kernel);
+ *   - the small-batch tile kernel (tv_tile_kernel: W <= 256, W % 4 == 0) when its
+ *     48-row tiles all fit on the CUs at once (few chains per GPU): ONE launch,
+ *     finalised by its last workgroup like the stream kernel;
  *   - otherwise (n_tv > 10 or H < 2, or kernel_variant 1) the temporally blocked
  *     band kernel (tv_main_kernel) followed by a small finaliser kernel
  *     (tv_finalise_kernel, <= 8 workgroups) that does the same.
@@ -108,7 +111,12 @@ typedef struct PsglaTvStep {
     int32_t launch_mask;      /* 0 or 3: both kernels; 1: tile kernel only (re-runs the same step:
                                  idempotent, for kernel timing); 2: finaliser only            */
     int32_t kernel_variant;   /* 0: auto (row-streaming pipeline when W % 4 == 0 and n_tv <= 10,
-                                 else temporally blocked bands); 1: force bands; 2: force stream */
+                                 else temporally blocked bands); 1: force bands; 2: force stream
+                                 (one workgroup barrier per pipeline step); 3: force stream with
+                                 point-to-point LDS progress waits instead of the barrier; 4: force
+                                 the small-batch tile kernel (W <= 256, W % 4 == 0, ldw == W).  Auto
+                                 picks the tile kernel when its tiles (one per workgroup, 48 rows
+                                 incl. n_tv halo rows) all fit on the CUs at once, else the stream */
     uint64_t* debug_stamps;   /* diagnostic builds only (-DPSGLA_STAMPS), else NULL: [workgroups][16][2]
                                  work / wait shader cycles per wave of the streaming kernel, then
                                  [steps][16][2] barrier arrival / release times of workgroup 0,
@@ -125,6 +133,10 @@ typedef struct PsglaTvStep {
 } PsglaTvStep;
 
 int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream);
+/* Which kernel psgla_tv_step launches for this descriptor (host-side query, launches nothing):
+ * 0 band kernel + finaliser, 1 row stream, 2 row stream with P2P waits, 3 small-batch tile kernel
+ * (one launch, finalised by its last workgroup); -1 if the descriptor is rejected. */
+int psgla_tv_step_kernel(const PsglaTvStep* d);
 
 /* ---------------------------------------------------------------------------------
  * psgla_tv_prox: TVDenoiser.forward(y, ths) on a (B,C,H,W) tensor, deepinv 0.2.1

@@ -64,6 +64,7 @@ _SIGNATURES = {
     "psgla_last_error": (ctypes.c_char_p, []),
     "psgla_tv_step": (c_i32, [ctypes.POINTER(PsglaTvStep), ctypes.POINTER(PsglaSchedule), c_vp]),
     "psgla_tv_prox": (c_i32, [ctypes.POINTER(PsglaTvProx), c_vp]),
+    "psgla_tv_step_kernel": (c_i32, [ctypes.POINTER(PsglaTvStep)]),
     "psgla_normal_fill": (c_i32, [c_vp, c_i32, c_i64, c_u64, c_i32, c_vp, c_i64, c_u32, c_vp]),
     "psgla_langevin_update": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i64, c_f, c_f, c_u64, c_i32, c_vp,
                                       c_i64, c_vp]),

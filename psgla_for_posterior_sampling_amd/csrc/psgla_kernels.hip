@@ -93,6 +93,8 @@ struct TvArgs {
     int split_wgs;                  // stream kernel: > 0 = row-split mode over this many workgroups
     int st_nsegs, st_seg_w, st_halo;  // stream kernel column segmentation (W > 256)
     int fin_inline;                 // stream kernel: 1 = the last workgroup finalises the step
+    int p2p;                        // stream kernel: 1 = point-to-point LDS progress waits instead of barriers
+    int tile_r;                     // > 0: small-batch tile kernel with tile_r rows per wave (one tile per workgroup)
     unsigned long long* stamps;     // diagnostic build only (PSGLA_STAMPS): per-wave work/wait cycles
 };
 
@@ -576,6 +578,10 @@ struct StreamShared {
     uint32_t fmk[SP_FRONT][2][WAVE];
     float4 bst[SP_BACK][2][2][WAVE];
     float red[SP_MAXSEG][SP_MAXST][2];
+    // P2P pipelines: prog[w] = steps of the pass whose shared-LDS work wave w has completed (its ring /
+    // Y-ring reads landed and writes performed); p2p_fail: a progress wait ran out (bounded spin)
+    uint32_t prog[16];
+    uint32_t p2p_fail;
 };
 
 typedef __attribute__((address_space(1))) const void* gptr_t;
@@ -668,6 +674,87 @@ __device__ __forceinline__ void step_barrier(Stamps& st) {
     (void)st;
     lds_barrier();
 #endif
+}
+
+// ---- point-to-point pipeline synchronisation (P2P variant) ----
+// Instead of one workgroup barrier per step, every wave publishes its progress in LDS (prog[w] = T + 1
+// once step T's ring reads have landed and its ring writes are performed: s_waitcnt lgkmcnt(0) first),
+// and waits only for the waves whose data it reads (RAW: the producer reached step T) or whose slot it
+// overwrites (WAR: the consumer reached step T) -- every dependency of step T is on step T - 1 work, so
+// neighbours drift by at most about one step and nothing can deadlock.  Waves that have no shared LDS
+// work in a step publish at its end.  A wait is a bounded poll (s_sleep between polls); on a timeout
+// the pass stops waiting (p2p_fail, reported through arrive[1]) so the grid still drains.
+constexpr uint32_t P2P_SPIN_MAX = 1u << 17;
+// issue priorities of the roles in the P2P pipeline (the barrier pipeline: front 0, stages 1, back 3)
+#ifndef PSGLA_P2P_PRIO_FRONT
+#define PSGLA_P2P_PRIO_FRONT 3
+#endif
+#ifndef PSGLA_P2P_PRIO_STAGE
+#define PSGLA_P2P_PRIO_STAGE 1
+#endif
+#ifndef PSGLA_P2P_PRIO_BACK
+#define PSGLA_P2P_PRIO_BACK 2
+#endif
+template <bool P2P>
+__device__ __forceinline__ void p2p_wait(StreamShared& sh, int wv, int target) {
+    if constexpr (P2P) {
+        if (target <= 0) return;
+        const uint32_t tg = (uint32_t)target;
+        for (uint32_t spins = 0;; ++spins) {
+            const uint32_t v = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&sh.prog[wv]);
+            if (v >= tg) break;
+            if (spins >= P2P_SPIN_MAX || *(volatile uint32_t*)&sh.p2p_fail) {
+                *(volatile uint32_t*)&sh.p2p_fail = 1u;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        asm volatile("" ::: "memory");
+    } else {
+        (void)sh; (void)wv; (void)target;
+    }
+}
+// A wave's LDS operations are performed in issue order (LDS-only lgkmcnt retires in order), so a
+// progress word written after a step's ring writes / reads is seen only once they are performed: the
+// publish needs no wait, and a progress word read BEFORE a row's ring reads ("peek"), if it already
+// shows the producer's step, proves those reads saw the row -- the poll's latency overlaps them.
+template <bool P2P>
+__device__ __forceinline__ void p2p_publish(StreamShared& sh, int w, int value) {
+    if constexpr (P2P) {
+        asm volatile("" ::: "memory");
+        *(volatile uint32_t*)&sh.prog[w] = (uint32_t)value;
+        asm volatile("" ::: "memory");
+    } else {
+        (void)sh; (void)w; (void)value;
+    }
+}
+template <bool P2P>
+__device__ __forceinline__ uint32_t p2p_peek(StreamShared& sh, int wv) {
+    if constexpr (P2P) {
+        const uint32_t v = *(volatile uint32_t*)&sh.prog[wv];
+        asm volatile("" ::: "memory");
+        return v;
+    } else {
+        (void)sh; (void)wv;
+        return 0xFFFFFFFFu;
+    }
+}
+// true when a peeked progress word already satisfies `target` (wave-uniform)
+template <bool P2P>
+__device__ __forceinline__ bool p2p_ok(uint32_t peeked, int target) {
+    if constexpr (P2P) return target <= 0 || __builtin_amdgcn_readfirstlane(peeked) >= (uint32_t)target;
+    else return true;
+}
+// end of step T: the workgroup barrier (barrier pipelines) or, if not done mid-step, the publish (P2P)
+template <bool P2P>
+__device__ __forceinline__ void step_end(StreamShared& sh, Stamps& st, int w, int T, bool published) {
+    if constexpr (P2P) {
+        if (!published) p2p_publish<true>(sh, w, T + 1);
+        (void)st;
+    } else {
+        (void)sh; (void)w; (void)T; (void)published;
+        step_barrier(st);
+    }
 }
 
 struct StepInfo {
@@ -917,9 +1004,10 @@ __device__ __forceinline__ void stage_phase_b(const TvArgs& a, const StageRow& r
 // Segment edges (split mode): the first row of a segment has no row above (its primal
 // uses u0 = 0 above) and the last has no row below (its dual has no vertical difference);
 // the rel-err partial sums are flushed per segment (different segments may be different chains).
-template <bool EXACT, bool TRK, bool GEN>
-__device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, const RowMap& rm, int k, int nsteps,
-                                           int Qk, int lane, int lastk, int nreal, bool core, Stamps& stp) {
+template <bool EXACT, bool TRK, bool GEN, bool P2P>
+__device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, const RowMap& rm, int k, int n,
+                                           int nsteps, int Qk, int lane, int lastk, int nreal, bool core,
+                                           Stamps& stp) {
     // GEN: the lane's columns change with the column segment of the row (row split over virtual
     // planes): lastk / nreal / core follow the primal row's segment; each row carries its lastk
     // to its dual (StageRow.lk)
@@ -934,6 +1022,17 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
     };
     const int Q = Qk;                    // rows this stage runs (the stream's, bottom-halo trimmed)
     const int tbeg = 1 + 3 * k;          // step of lookahead row 0
+    // P2P: this wave, the producer of ring k-1 (stage k-1; for k = 1 the front wave of the row) and the
+    // consumer of ring k (stage k+1; for k = n the back wave of the row)
+    const int wme = SP_FRONT + k - 1;
+    auto raw_wave = [&](int j) { return k == 1 ? (j & 3) : wme - 1; };   // wrote ring k-1 row j
+    auto war_wave = [&](int i) { return k < n ? wme + 1 : SP_FRONT + n + ((i - 2) & 1); };  // read row i - 2
+    auto wait_raw = [&](int j) {          // before reading ring k-1 row j (step T = tbeg + j)
+        p2p_wait<P2P>(sh, raw_wave(j), tbeg + j);
+    };
+    auto wait_war = [&](int i, int T) {   // before writing ring k row i (its slot's previous row i - 2)
+        if (i - 2 >= 0) p2p_wait<P2P>(sh, war_wave(i), T);
+    };
     StageRow RA, RB, RC;
     const float zero[CPL] = {0.f, 0.f, 0.f, 0.f};
     float lsd = 0.f, lsn = 0.f;          // rel-err partial sums of segment sacc (core rows)
@@ -958,7 +1057,7 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
         if (TRK && j >= qc0 && j < qc1) { lsd += rd; lsn += rn; }
     };
     int t = 0;
-    for (; t < tbeg; ++t) step_barrier(stp);
+    for (; t < tbeg; ++t) step_end<P2P>(sh, stp, wme, t, false);
     auto load_row = [&](int j, float4& X2, float4& U0, float4& U1, float4& YY) {
         const int sl = j & 1;
         X2 = sh.x2[k - 1][sl][lane];
@@ -975,22 +1074,36 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
     // rows 0 and 1: primal update only (segments hold >= 2 rows: row 1 never starts one)
     {
         float4 X2, U0, U1, YY;
+        wait_raw(0);
         load_row(0, X2, U0, U1, YY);
+        p2p_publish<P2P>(sh, wme, tbeg + 1);
         primal(0, X2, U0, U1, YY, zero, RA);
-        step_barrier(stp);
+        step_end<P2P>(sh, stp, wme, tbeg, true);
+        wait_raw(1);
         load_row(1, X2, U0, U1, YY);
+        p2p_publish<P2P>(sh, wme, tbeg + 2);
         primal(1, X2, U0, U1, YY, RA.u0, RB);
-        step_barrier(stp);
+        step_end<P2P>(sh, stp, wme, tbeg + 1, true);
         t += 2;
     }
     // middle rows j = 2..Q-1: dual update of row j-2 (p2) with z of row j-1 (p1), then primal of j
     auto middle = [&](int j, StageRow& p2, StageRow& p1, StageRow& cur) {
         float4 X2, U0, U1, YY;
+        const int T = tbeg + j;
+        // P2P: both progress words peeked ahead of the ring reads; checked where they matter
+        const uint32_t pk_raw = p2p_peek<P2P>(sh, raw_wave(j));
+        const uint32_t pk_war = p2p_peek<P2P>(sh, war_wave(j - 2));
         load_row(j, X2, U0, U1, YY);
         float un0[CPL], un1[CPL];
         if (!fprev) stage_phase_b<EXACT, true, GEN>(a, p2, p1.z, GEN ? p2.lk : lastk, un0, un1);
         else stage_phase_b<EXACT, false, GEN>(a, p2, zero, GEN ? p2.lk : lastk, un0, un1);   // row j-2 ends a segment
+        if (!p2p_ok<P2P>(pk_war, j - 4 >= 0 ? T : 0)) wait_war(j - 2, T);
         store_row(j - 2, p2, un0, un1);
+        if (!p2p_ok<P2P>(pk_raw, T)) {       // rare: the row was not there yet -- wait, read it again
+            wait_raw(j);
+            load_row(j, X2, U0, U1, YY);
+        }
+        p2p_publish<P2P>(sh, wme, T + 1);
         const bool fj = j == nb;
         if (fj) {                       // row j starts a new segment (split mode only)
             flush();
@@ -1002,7 +1115,7 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
             primal(j, X2, U0, U1, YY, p1.u0, cur);
         }
         fprev = fj;
-        step_barrier(stp);
+        step_end<P2P>(sh, stp, wme, tbeg + j, true);
     };
     int j = 2;
     for (; j + 2 < Q; j += 3) {
@@ -1016,11 +1129,13 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
     auto finish = [&](StageRow& r2, StageRow& r1) {
         float un0[CPL], un1[CPL];
         stage_phase_b<EXACT, true, GEN>(a, r2, r1.z, GEN ? r2.lk : lastk, un0, un1);
+        wait_war(Q - 2, tbeg + Q);
         store_row(Q - 2, r2, un0, un1);
-        step_barrier(stp);
+        step_end<P2P>(sh, stp, wme, tbeg + Q, false);
         stage_phase_b<EXACT, false, GEN>(a, r1, zero, GEN ? r1.lk : lastk, un0, un1);
+        wait_war(Q - 1, tbeg + Q + 1);
         store_row(Q - 1, r1, un0, un1);
-        step_barrier(stp);
+        step_end<P2P>(sh, stp, wme, tbeg + Q + 1, false);
     };
     const int rem = Q - j;              // 0, 1 or 2 middle rows left
     if (rem == 0) {
@@ -1034,7 +1149,7 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
         finish(RC, RA);
     }
     t += rem + 2;
-    for (; t < nsteps; ++t) step_barrier(stp);
+    for (; t < nsteps; ++t) step_end<P2P>(sh, stp, wme, t, false);
     flush();
 }
 
@@ -1043,11 +1158,16 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
 // pass and the rare early-stop recompute, each with its own register allocation.
 // GEN: the row pitch is not the image width (rows padded: W % 4 != 0) -- the last-column, norm
 // and noise-window handling of such rows, compiled only into the kernels that need it
-template <bool EXACT, bool ALPHA1, bool GEN>
+template <bool EXACT, bool ALPHA1, bool GEN, bool P2P>
 __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, const RowMap& rm, const int n,
                                             const bool track, const long long step, const bool fresh, Stamps& stp) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (scalar branches)
+    if constexpr (P2P) {                                   // progress counters of this pass start at 0
+        if (threadIdx.x < 16) sh.prog[threadIdx.x] = 0u;
+        if (threadIdx.x == 0) sh.p2p_fail = 0u;
+        lds_barrier();
+    }
     const int H = a.H, W = a.W, C = a.C;
     const int L = a.ldw;                                   // row pitch (memory); W: the image's width
     const size_t HW = (size_t)H * L;                       // plane pitch
@@ -1131,7 +1251,9 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         for (int t = 0; t < nsteps; ++t) step_barrier(stp);   // diagnostic timing build only
         if (nsteps >= 0) return;
 #endif
+        if (P2P) __builtin_amdgcn_s_setprio(PSGLA_P2P_PRIO_FRONT);
         for (int t = 0; t < nsteps; ++t) {
+                bool pub = false;
                 // ======================= FRONT =======================
                 const int p = (t + 4 - fw) & 3;
                 const int q = t - p;
@@ -1175,6 +1297,9 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                         }
                     } else {
                         STAMP_START(stp);
+                        // P2P: the slots this phase overwrites (see below), peeked ahead
+                        const uint32_t pk_s1 = p2p_peek<P2P>(sh, SP_FRONT);
+                        const uint32_t pk_sn = p2p_peek<P2P>(sh, SP_FRONT + n - 1);
                         wait_vm<ALPHA1 ? 4 : 4>();   // row q's loads landed; parts 0-2 of row q + 4 may fly
                         STAMP_SEG(stp, 0);
                         const int bi = (q >> 2) & 1;
@@ -1207,10 +1332,20 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                         if (!okf) x2s = zero4;
                         const int s0 = q & 1;
                         STAMP_SEG(stp, 1);
+                        // P2P: ring 0 slot (previous row q - 2, read by stage 1 at step t - 1) and Y-ring
+                        // slot (row q - 32: read by the stages up to step t - 4, by the back at t - 1)
+                        if (!p2p_ok<P2P>(pk_s1, t)) p2p_wait<P2P>(sh, SP_FRONT, t);
+                        if (!p2p_ok<P2P>(pk_sn, t - 33 + 3 * n)) p2p_wait<P2P>(sh, SP_FRONT + n - 1, t - 33 + 3 * n);
+                        if (!ALPHA1) {
+                            p2p_wait<P2P>(sh, SP_FRONT + n, t);
+                            p2p_wait<P2P>(sh, SP_FRONT + n + 1, t);
+                        }
                         sh.x2[0][s0][lane] = x2s;
                         sh.u0[0][s0][lane] = fresh ? zero4 : make_float4(fU0.x, fU0.z, fU1.x, fU1.z);
                         sh.u1[0][s0][lane] = fresh ? zero4 : make_float4(fU0.y, fU0.w, fU1.y, fU1.w);
                         sh.y[q & (SP_YRING - 1)][lane] = Y4;
+                        p2p_publish<P2P>(sh, fw, t + 1);
+                        pub = true;
                         STAMP_SEG(stp, 2);
                         // the wave's next rows: noise row q + 4, DMA of row q + 8... issued as q + 4
                         front_issue(3, q + 4, rc_dma);
@@ -1219,7 +1354,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                         STAMP_SEG(stp, 3);
                     }
                 }
-            step_barrier(stp);
+            step_end<P2P>(sh, stp, fw, t, pub);
         }
     } else if (role == 1) {
         // ---------------- STAGE (one inner TV iteration per wave) ----------------
@@ -1228,12 +1363,13 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         // select: the DPP shift feeds 0 at lane 0 and TV keeps those dual components exactly 0.
         const int lastk = W - 1 - gj0;                    // in 0..3 on the lane holding column W-1
         const int nreal = min(CPL, max(0, W - gj0));      // real (non-pitch-padding) columns of the lane
-        __builtin_amdgcn_s_setprio(1);
+        if (P2P) __builtin_amdgcn_s_setprio(PSGLA_P2P_PRIO_STAGE);
+        else __builtin_amdgcn_s_setprio(1);
         const int qk = stage_rows(k_st);
-        if (trk) stage_loop<EXACT, true, GEN>(a, sh, rm, k_st, nsteps, qk, lane, lastk, nreal, core, stp);
-        else stage_loop<EXACT, false, GEN>(a, sh, rm, k_st, nsteps, qk, lane, lastk, nreal, core, stp);
+        if (trk) stage_loop<EXACT, true, GEN, P2P>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core, stp);
+        else stage_loop<EXACT, false, GEN, P2P>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core, stp);
     } else if (role == 3) {
-        for (int t = 0; t < nsteps; ++t) step_barrier(stp);
+        for (int t = 0; t < nsteps; ++t) step_end<P2P>(sh, stp, w, t, false);
     } else {
 #ifdef PSGLA_ABL_NOBACK
         for (int t = 0; t < nsteps; ++t) step_barrier(stp);   // diagnostic timing build only
@@ -1244,7 +1380,8 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         // issue priority: back > stages > front.  The back waves are the youngest of the
         // workgroup (lowest age priority) yet close every step (its last arrivals, measured);
         // raising them, then the stages, cut the step by 9 % (A/B).
-        __builtin_amdgcn_s_setprio(3);
+        if (P2P) __builtin_amdgcn_s_setprio(PSGLA_P2P_PRIO_BACK);
+        else __builtin_amdgcn_s_setprio(3);
         const StepInfo si = step_info(a, step, a.mean[par_out]);
         const float* mean_in = a.mean[par_in];
         const float* sq_in = a.sq[par_in];
@@ -1293,13 +1430,22 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         back_issue(bw + 2, rc_dma);
         int c1 = 2, c2 = 0;
         for (int t = 0; t < nsteps; ++t) {
+                bool pub = false;
                 // ======================= BACK =======================
                 const int q = t - 4 - 3 * n;
                 if (q >= 0 && q < Qb && (q & 1) == bw) {
                     const int sl = q & 1;
-                    const float4 X2 = sh.x2[n][sl][lane];
-                    const float4 U0 = sh.u0[n][sl][lane];
-                    const float4 U1 = sh.u1[n][sl][lane];
+                    // stage n wrote ring n row q at step t - 1 (P2P: peeked ahead of the reads)
+                    const uint32_t pk = p2p_peek<P2P>(sh, SP_FRONT + n - 1);
+                    float4 X2 = sh.x2[n][sl][lane];
+                    float4 U0 = sh.u0[n][sl][lane];
+                    float4 U1 = sh.u1[n][sl][lane];
+                    if (!p2p_ok<P2P>(pk, t)) {
+                        p2p_wait<P2P>(sh, SP_FRONT + n - 1, t);
+                        X2 = sh.x2[n][sl][lane];
+                        U0 = sh.u0[n][sl][lane];
+                        U1 = sh.u1[n][sl][lane];
+                    }
                     float4 Xo = X2;
                     if (!ALPHA1) {
                         const float4 YY = sh.y[q & (SP_YRING - 1)][lane];
@@ -1337,6 +1483,8 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                     // all LDS reads of this row (ring + staging) done before the staging
                     // buffer is re-targeted by the next DMA
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    p2p_publish<P2P>(sh, SP_FRONT + n + bw, t + 1);
+                    pub = true;
                     const RowCursor rc = rc_cur;
                     cursor_advance(rm, rc_cur, 2);
                     if (q + 4 < Q) cursor_advance(rm, rc_dma, 2);
@@ -1368,7 +1516,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                     flush_held();
                     hold = false;
                 }
-            step_barrier(stp);
+            step_end<P2P>(sh, stp, SP_FRONT + n + bw, t, pub);
         }
         if (hold) flush_held();
     }
@@ -1387,7 +1535,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
     // early-stop test, per chain); the tracking stages wrote sh.red[segment][k - 1]
 }
 
-template <bool EXACT, bool ALPHA1, bool GEN>
+template <bool EXACT, bool ALPHA1, bool GEN, bool P2P>
 __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     __shared__ StreamShared sh;
     __shared__ int s_stop[MAXG];
@@ -1404,7 +1552,11 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     {
         RowMap rm;
         build_rowmap(a, blockIdx.x, rm);
-        stream_pass<EXACT, ALPHA1, GEN>(a, sh, rm, a.n_tv, true, step, fresh, stp);
+        stream_pass<EXACT, ALPHA1, GEN, P2P>(a, sh, rm, a.n_tv, true, step, fresh, stp);
+        if (P2P) {
+            lds_barrier();
+            if (threadIdx.x == 0 && sh.p2p_fail) atomicOr(a.arrive + 1, 1);   // diagnostic: a wait timed out
+        }
         if (!a.fin_inline) return;        // main-pass-only launch (kernel timing): no side effects
         // rel_err partial sums of this stream -> global, per segment's chain (deepinv's
         // early-stop test, per chain); the tracking stages wrote sh.red[segment][k - 1]
@@ -1477,7 +1629,343 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
         RowMap rm;
         plane_rowmap(a.H, item, rm);                 // the virtual plane (plane, column segment)
         const int nstop = __builtin_amdgcn_readfirstlane(s_stop[plane / C]);
-        stream_pass<EXACT, ALPHA1, GEN>(a, sh, rm, nstop, false, step, fresh, stp);
+        stream_pass<EXACT, ALPHA1, GEN, P2P>(a, sh, rm, nstop, false, step, fresh, stp);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.B * a.n_tv * 2; i += blockDim.x) a.norms[i] = 0.0;
+    if (threadIdx.x == 0) {
+        *a.arrive = 0;
+        if (a.fresh_dev) *a.fresh_dev = 0;
+        if (a.advance_step && a.d_step) *a.d_step = *a.d_step + 1;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Small-batch fused step ("tile" variant, kernel_variant 4 / auto for small batches).
+//
+// Strong scaling gives each GPU 64/N chains: at 8 chains the row stream of a CU is ~24 core rows
+// plus 2 x n_tv halo rows plus a 34-step pipeline fill, so the streaming pipeline spends most of
+// a step filling and draining.  Here every (plane, band) tile is ONE workgroup and all tiles are
+// resident at once: 16 waves x R rows x 256 columns (4 per lane) held in registers through all
+// inner TV iterations (temporally blocked, n_tv halo rows recomputed by the neighbour bands, as
+// the band kernel), with every load of the tile issued up front (the Philox / Box-Muller noise is
+// computed while they fly; mean / sq LDS-DMA'd straight into LDS), 16-byte accumulator updates and
+// the step finalised by the last workgroup (no second launch).  The per-element arithmetic is
+// the stream kernel's in both modes (exact: bit-identical to the oracle; fast: bit-identical to
+// the fast stream kernel).  W <= 256, W % 4 == 0; halos only at cuts inside a plane.
+// ---------------------------------------------------------------------------------------
+template <int R>
+struct TileShared {
+    float4 zrow[TV_NW][WAVE];          // first-row z of each wave (read by the wave above)
+    float4 urow[TV_NW][WAVE];          // last-row u2[..., 0] of each wave (read by the wave below)
+    float4 mst[TV_NW * R][2][WAVE];    // mean / sq rows of the tile (LDS-DMA at the start)
+    float red[MAXIT][TV_NW][2];        // per-wave rel_err partial sums
+    int s_stop[MAXG];
+    int s_flag, s_item, s_next;
+};
+
+template <bool EXACT, bool ALPHA1, int R>
+__device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int plane, int band, int n_it,
+                                        bool track, long long step, bool fresh) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int H = a.H, W = a.W, C = a.C, h = a.halo;
+    const int b = plane / C, c = plane - b * C;
+    const int r0 = band * a.band_h, r1 = min(H, r0 + a.band_h);
+    const int e0 = max(0, r0 - h), e1 = min(H, r1 + h);
+    const int gj0 = CPL * lane;
+    const int gjc = min(gj0, W - CPL);                 // DMA source column (every lane in bounds)
+    const bool colok = gj0 < W;
+    const size_t HW = (size_t)H * W;
+    const size_t E = (size_t)C * HW;
+    const size_t BE = (size_t)a.B * E;
+    const size_t poff = (size_t)plane * HW;
+    const int par_in = (int)(step & 1), par_out = (int)((step + 1) & 1);
+    const StepInfo si = step_info(a, step, a.mean[par_out]);
+    const bool need_prev = si.acc && !si.first;
+    const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+
+    float x2[R][CPL], u0[R][CPL], u1[R][CPL], z[R][CPL], yv[R][CPL];
+    int gi[R];
+    bool rv[R], core[R];
+    // ---- 1. every load of the tile in flight: state and observation to registers, mean / sq by DMA
+    float4 fX[R], fY[R], fU0[R], fU1[R], fXS[R];
+    uint32_t fM[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        gi[r] = e0 + w * R + r;
+        rv[r] = gi[r] < e1;
+        core[r] = gi[r] >= r0 && gi[r] < r1;
+        fX[r] = fY[r] = fU0[r] = fU1[r] = fXS[r] = zero4;
+        fM[r] = 0u;
+        if (rv[r] && colok) {
+            const size_t base = poff + (size_t)gi[r] * W + gj0;
+            fX[r] = ld4(a.x[par_in] + base);
+            fY[r] = ld4(a.yobs + (size_t)b * a.y_cs + (size_t)c * HW + (size_t)gi[r] * W + gj0);
+            fM[r] = *reinterpret_cast<const uint32_t*>(a.mask + (size_t)b * a.m_cs + (size_t)gi[r] * W + gj0);
+            if (!fresh) {
+                fU0[r] = ld4(a.u2[par_in] + 2 * base);
+                fU1[r] = ld4(a.u2[par_in] + 2 * base + 4);
+                if (!ALPHA1) fXS[r] = ld4(a.x2[par_in] + base);
+            }
+        }
+    }
+    if (need_prev && n_it >= 0) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (rv[r] && core[r]) {
+                const size_t base = poff + (size_t)gi[r] * W + gjc;
+                glds16(a.mean[par_in] + base, &sh.mst[w * R + r][0][0]);
+                glds16(a.sq[par_in] + base, &sh.mst[w * R + r][1][0]);
+            }
+        }
+    }
+    // ---- 2. the noise of the tile's rows (no memory dependence: overlaps the loads)
+    float Zn[R][CPL];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const size_t e = ((size_t)c * H + (rv[r] ? gi[r] : 0)) * W + gj0;
+        normal_quad(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)(e >> 2), Zn[r]);
+    }
+    // ---- 3. data term Y = (X + c1 g) + c2 Z, TV start state
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const bool ok = rv[r] && colok;
+        const float X[CPL] = {fX[r].x, fX[r].y, fX[r].z, fX[r].w};
+        const float yo[CPL] = {fY[r].x, fY[r].y, fY[r].z, fY[r].w};
+        const float mk[CPL] = {(float)(fM[r] & 0xFFu), (float)((fM[r] >> 8) & 0xFFu), (float)((fM[r] >> 16) & 0xFFu),
+                               (float)(fM[r] >> 24)};
+        const float xs[CPL] = {fXS[r].x, fXS[r].y, fXS[r].z, fXS[r].w};
+        const float us0[CPL] = {fU0[r].x, fU0[r].z, fU1[r].x, fU1[r].z};
+        const float us1[CPL] = {fU0[r].y, fU0[r].w, fU1[r].y, fU1[r].w};
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            float Y;
+            if (EXACT) {
+                const float g = (-mk[k] * (X[k] - yo[k])) / a.sigma2;
+                Y = (X[k] + a.c1 * g) + a.c2 * Zn[r][k];
+            } else {
+                const float g = (mk[k] * (yo[k] - X[k])) * a.inv_sigma2;
+                Y = __builtin_fmaf(a.c2, Zn[r][k], __builtin_fmaf(a.c1, g, X[k]));
+            }
+            yv[r][k] = ok ? Y : 0.f;
+            x2[r][k] = ok ? (fresh ? Y : (ALPHA1 ? X[k] : xs[k])) : 0.f;
+            u0[r][k] = (ok && !fresh) ? us0[k] : 0.f;
+            u1[r][k] = (ok && !fresh) ? us1[k] : 0.f;
+            z[r][k] = 0.f;
+        }
+    }
+    sh.urow[w][lane] = make_float4(u0[R - 1][0], u0[R - 1][1], u0[R - 1][2], u0[R - 1][3]);
+    __syncthreads();
+
+    // ---- 4. inner TV iterations (deepinv 0.2.1 TVDenoiser, the stream kernel's arithmetic)
+    const bool lastlane = gj0 + CPL == W;              // holds column W-1: no forward difference there
+    for (int it = 0; it < n_it; ++it) {
+        const bool trk = track && it >= trk_lo(a) && it <= trk_hi(a);
+        float sd = 0.f, sn = 0.f;
+        // primal: x = prox_tau_fx(x2 - tau nabla^T u2, Y); z = 2x - x2; x2 += rho (x - x2)
+        const float4 up = (w > 0) ? sh.urow[w - 1][lane] : zero4;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const float u1l = __int_as_float(
+                __builtin_amdgcn_update_dpp(0, __float_as_int(u1[r][CPL - 1]), 0x138 /* wave_shr:1 */, 0xF, 0xF, true));
+            const bool top = gi[r] == 0;
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const float pu = top ? 0.f : ((r > 0) ? u0[r - 1][k] : f4get(up, k));
+                const float u1left = (k > 0) ? u1[r][k - 1] : u1l;
+                const float tt = ((pu - u0[r][k]) - u1[r][k]) + u1left;
+                const float xo = x2[r][k];
+                float xv, zv, xn;
+                if (EXACT) {
+                    xv = ((xo - a.tau * tt) + a.tau * yv[r][k]) / a.opt;
+                    zv = 2.0f * xv - xo;
+                    xn = xo + a.rho * (xv - xo);
+                } else {
+                    xv = __builtin_fmaf(a.tau, yv[r][k] - tt, xo) * a.inv_opt;
+                    zv = __builtin_fmaf(2.0f, xv, -xo);
+                    xn = __builtin_fmaf(a.rho, xv - xo, xo);
+                }
+                if (trk) {
+                    const bool cnt = core[r] && rv[r] && colok;
+                    if (EXACT) {
+                        const float d = cnt ? xo - xn : 0.f;
+                        const float q = cnt ? xn + 1e-12f : 0.f;
+                        sd = __builtin_fmaf(d, d, sd);
+                        sn = __builtin_fmaf(q, q, sn);
+                    } else {
+                        const float d = cnt ? xv - xo : 0.f;
+                        const float q = cnt ? xn : 0.f;
+                        sd = __builtin_fmaf(d, d, sd);
+                        sn = __builtin_fmaf(q, q, sn);
+                    }
+                }
+                z[r][k] = zv;
+                x2[r][k] = xn;
+            }
+        }
+        sh.zrow[w][lane] = make_float4(z[0][0], z[0][1], z[0][2], z[0][3]);
+        if (trk) {
+            sd = wave_sum(sd);
+            sn = wave_sum(sn);
+            if (!EXACT) sd *= a.rho * a.rho;          // fast sums hold (x - x2_prev)^2
+            if (lane == 0) { sh.red[it][w][0] = sd; sh.red[it][w][1] = sn; }
+        }
+        __syncthreads();
+        // dual: u = prox_sigma_g_conj(u2 + sigma nabla z, ths); u2 += rho (u - u2)
+        const float4 dn = (w < TV_NW - 1) ? sh.zrow[w + 1][lane] : zero4;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const float zr3 = __int_as_float(
+                __builtin_amdgcn_update_dpp(0, __float_as_int(z[r][0]), 0x130 /* wave_shl:1 */, 0xF, 0xF, true));
+            const bool down = gi[r] < H - 1;
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const float zc = z[r][k];
+                const float zd = (r < R - 1) ? z[r + 1][k] : f4get(dn, k);
+                const float zr = (k < CPL - 1) ? z[r][k + 1] : zr3;
+                const float g0 = down ? (zd - zc) : 0.0f;
+                float g1 = zr - zc;
+                if (k == CPL - 1) g1 = lastlane ? 0.0f : g1;
+                const float uo0 = u0[r][k], uo1 = u1[r][k];
+                if (EXACT) {
+                    const float v0 = uo0 + a.sig_tv * g0;
+                    const float v1 = uo1 + a.sig_tv * g1;
+                    const float nrm = sqrtf(v0 * v0 + v1 * v1) / a.ths;
+                    const float dd = fmaxf(nrm, 1.0f);
+                    u0[r][k] = uo0 + a.rho * (v0 / dd - uo0);
+                    u1[r][k] = uo1 + a.rho * (v1 / dd - uo1);
+                } else {
+                    const float v0 = __builtin_fmaf(a.sig_tv, g0, uo0);
+                    const float v1 = __builtin_fmaf(a.sig_tv, g1, uo1);
+                    const float s2 = __builtin_fmaf(v0, v0, v1 * v1);
+                    const float f = fminf(1.0f, a.ths * __builtin_amdgcn_rsqf(s2));
+                    u0[r][k] = __builtin_fmaf(a.rho, __builtin_fmaf(v0, f, -uo0), uo0);
+                    u1[r][k] = __builtin_fmaf(a.rho, __builtin_fmaf(v1, f, -uo1), uo1);
+                }
+            }
+        }
+        sh.urow[w][lane] = make_float4(u0[R - 1][0], u0[R - 1][1], u0[R - 1][2], u0[R - 1][3]);
+        __syncthreads();
+    }
+    // ---- 5. rel_err partial sums -> the chain's norms (one fp64 atomic per iteration and workgroup)
+    if (track) {
+        const int t = threadIdx.x;
+        if (t >= trk_lo(a) && t <= trk_hi(a) && t < n_it) {
+            double sd = 0.0, sn = 0.0;
+            for (int ww = 0; ww < TV_NW; ++ww) { sd += sh.red[t][ww][0]; sn += sh.red[t][ww][1]; }
+            atomicAdd(&a.norms[((size_t)b * a.n_tv + t) * 2], sd);
+            atomicAdd(&a.norms[((size_t)b * a.n_tv + t) * 2 + 1], sn);
+        }
+    }
+    // ---- 6. the core rows out: X, u2 (x2), accumulators / block means, sample
+    if (need_prev) wait_vm0();                         // this wave's mean / sq DMA landed
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (!(rv[r] && core[r] && colok)) continue;
+        const size_t base = poff + (size_t)gi[r] * W + gj0;
+        float Xo[CPL];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+            Xo[k] = ALPHA1 ? x2[r][k] : (1.0f - a.alpha) * yv[r][k] + a.alpha * x2[r][k];
+        const float4 X4 = make_float4(Xo[0], Xo[1], Xo[2], Xo[3]);
+        st_nt(a.x[par_out] + base, X4);
+        float* u2o = a.u2[par_out] + 2 * base;
+        st_nt(u2o, make_float4(u0[r][0], u1[r][0], u0[r][1], u1[r][1]));
+        st_nt(u2o + 4, make_float4(u0[r][2], u1[r][2], u0[r][3], u1[r][3]));
+        if (!ALPHA1) st_nt(a.x2[par_out] + base, make_float4(x2[r][0], x2[r][1], x2[r][2], x2[r][3]));
+        if (si.acc) {
+            float4 bm = zero4, bq = zero4;
+            if (need_prev) {
+                bm = sh.mst[w * R + r][0][lane];
+                bq = sh.mst[w * R + r][1][lane];
+            }
+            const float ms[CPL] = {bm.x, bm.y, bm.z, bm.w};
+            const float qs[CPL] = {bq.x, bq.y, bq.z, bq.w};
+            float m[CPL], q[CPL];
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                if (si.first) {
+                    m[k] = si.cb * Xo[k];
+                    q[k] = si.cb * (Xo[k] * Xo[k]);
+                } else {
+                    m[k] = si.ca * ms[k] + si.cb * Xo[k];
+                    q[k] = si.ca * qs[k] + si.cb * (Xo[k] * Xo[k]);
+                }
+            }
+            const float4 M4 = make_float4(m[0], m[1], m[2], m[3]);
+            const float4 Q4 = make_float4(q[0], q[1], q[2], q[3]);
+            if (si.blockend) {
+                st_nt(a.blocks + (size_t)si.blk * BE + base, M4);
+                st_nt(a.blocks2 + (size_t)si.blk * BE + base, Q4);
+            } else if (si.liveout) {
+                st_nt(a.mean[par_out] + base, M4);
+                st_nt(a.sq[par_out] + base, Q4);
+            }
+        }
+        if (si.sample) st_nt(a.samples + (size_t)si.sidx * BE + base, X4);
+    }
+}
+
+template <bool EXACT, bool ALPHA1, int R>
+__global__ void __launch_bounds__(TV_THREADS) tv_tile_kernel(const TvArgs a) {
+    __shared__ TileShared<R> sh;
+    const long long step = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
+    const bool fresh = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
+    const int P = a.B * a.C;
+    const int T = a.nbands;
+    {
+        // all bands of a plane on one XCD (blocks x and x + 8 share one): their halo rows hit its L2
+        const int x = blockIdx.x, xcd = x & 7, k = x >> 3;
+        const int plane = (k / T) * 8 + xcd;
+        const int band = k - (k / T) * T;
+        if (plane < P) sb_tile<EXACT, ALPHA1, R>(a, sh, plane, band, a.n_tv, true, step, fresh);
+    }
+    if (!a.fin_inline) return;
+    // ---- step finalisation by the last workgroup to arrive (as tv_stream_kernel) ----
+    wait_vm0();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const int old = __hip_atomic_fetch_add(a.arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sh.s_flag = (old == (int)gridDim.x - 1) ? 1 : 0;
+        if (sh.s_flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    wait_vm0();
+    __syncthreads();
+    if (!sh.s_flag) return;
+    const int G = a.B;
+    for (int g = threadIdx.x; g < G; g += blockDim.x) sh.s_stop[g] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < G * MAXIT; i += blockDim.x) {
+        const int g = i / MAXIT, t = i - g * MAXIT;
+        if (t >= trk_lo(a) && t <= trk_hi(a) && t < a.n_tv) {
+            const double nd = a.norms[((size_t)g * a.n_tv + t) * 2];
+            const double nn = a.norms[((size_t)g * a.n_tv + t) * 2 + 1];
+            const float rel = (float)sqrt(nd) / (float)sqrt(nn);
+            if (rel < a.tol) atomicOr(&sh.s_stop[g], 1 << t);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) sh.s_item = 0;
+    __syncthreads();
+    for (int g = threadIdx.x; g < G; g += blockDim.x) {
+        const int m = sh.s_stop[g];
+        sh.s_stop[g] = m ? (__ffs(m) - 1) + 1 : a.n_tv;
+        if (m) sh.s_item = 1;
+    }
+    __syncthreads();
+    if (sh.s_item) {
+        // rare: redo every tile of a stopped chain with the stopped iteration count (inputs intact)
+        for (int item = 0; item < P * T; ++item) {
+            const int plane = item / T, band = item - plane * T;
+            const int nstop = __builtin_amdgcn_readfirstlane(sh.s_stop[plane / a.C]);
+            if (nstop < a.n_tv) {
+                sb_tile<EXACT, ALPHA1, R>(a, sh, plane, band, nstop, false, step, fresh);
+                wait_vm0();
+                __syncthreads();
+            }
+        }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < a.B * a.n_tv * 2; i += blockDim.x) a.norms[i] = 0.0;
@@ -2092,6 +2580,26 @@ static int choose_split(long long P, int H, int h, int req, int* out) {
     return 0;
 }
 
+// Small-batch tile kernel geometry: R rows per wave (tile = 16 R rows incl. n_tv halo rows at cuts inside
+// a plane), equal bands per plane.  Returns the number of workgroups (planes rounded up to 8 -- the
+// XCD-aware order -- times bands), 0 if the shape does not fit (W > 256 or W % 4, halo too large).
+static int tile_geometry(int P, int H, int W, int h, int R, int* band_h, int* nbands) {
+    if (W > TV_COLS || (W & 3) || R < 2 || R > 3) return 0;
+    const int rows = TV_NW * R;
+    int nb, bh;
+    if (H <= rows) {
+        nb = 1; bh = H;
+    } else {
+        const int core = rows - 2 * h;
+        if (core < 1) return 0;
+        nb = (H + core - 1) / core;
+        bh = (H + nb - 1) / nb;
+    }
+    *band_h = bh;
+    *nbands = nb;
+    return ((P + 7) / 8) * 8 * nb;
+}
+
 // Column segments of the streaming kernel: equal core widths (multiples of 4) cut from the image
 // width W; segment s's wave covers columns [f0, f0 + 256) with f0 = (cc0 - h) & ~3 (cc0 = s * seg_w),
 // which must reach cc1 + h for interior cuts (the TV dependency cone) and the row pitch L at the
@@ -2120,14 +2628,32 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
     const int P = a.B * a.C;
     if (mask == 0) mask = 3;
     if (mask & 1) {
+        if (FRONT == FRONT_INPAINT && a.tile_r > 0) {
+            TvArgs s = a;
+            s.fin_inline = (mask & 2) ? 1 : 0;
+            const int grid = ((P + 7) / 8) * 8 * s.nbands;
+            if (s.tile_r == 2)
+                hipLaunchKernelGGL((tv_tile_kernel<EXACT, ALPHA1, 2>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+            else
+                hipLaunchKernelGGL((tv_tile_kernel<EXACT, ALPHA1, 3>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+            return launch_check("tv_tile_kernel");
+        }
         if (FRONT == FRONT_INPAINT && a.stream) {
             TvArgs s = a;
             s.fin_inline = (mask & 2) ? 1 : 0;
             const int grid = s.split_wgs > 0 ? s.split_wgs : P * s.st_nsegs;   // virtual planes
-            if (s.ldw == s.W && s.st_nsegs == 1)
-                hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1, false>), dim3(grid), dim3(TV_THREADS), 0, st, s);
-            else
-                hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1, true>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+            const bool gen = !(s.ldw == s.W && s.st_nsegs == 1);
+            if (s.p2p) {
+                if (!gen)
+                    hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1, false, true>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+                else
+                    hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1, true, true>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+            } else {
+                if (!gen)
+                    hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1, false, false>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+                else
+                    hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1, true, false>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+            }
             int rc = launch_check("tv_stream_kernel");
             if (rc) return rc;
             return 0;                    // finalised in-kernel (or main pass only)
@@ -2153,6 +2679,52 @@ static int check_tv_common(int B, int C, int H, int W, int n_tv) {
     if (n_tv < 0 || n_tv > MAXIT)
         return fail(0, "psgla: n_it_max outside [0, PSGLA_TV_MAX_FUSED_IT] for the fused TV kernel");
     if (H > TV_ROWS && TV_ROWS - 2 * n_tv < 1) return fail(0, "psgla: TV halo too large");
+    return 0;
+}
+
+// Which fused-step kernel psgla_tv_step launches for a descriptor, and its geometry in `a` (B, C, H, W,
+// ldw and n_tv of `a` set): 0 band kernel (+ finaliser), 1 row stream, 2 row stream with P2P waits,
+// 3 small-batch tile kernel; -1 with g_sel_err on a shape the requested variant does not support.
+static thread_local const char* g_sel_err = "";
+static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
+    a.halo = d->n_tv;
+    tv_tiling(a);
+    const bool streamable = (a.ldw % 4 == 0) && d->n_tv >= 1 && d->n_tv <= SP_MAXST && d->H >= 2 &&
+                            stream_segments(a.W, a.ldw, d->n_tv, nullptr) > 0;
+    a.stream = streamable && d->kernel_variant != 1;
+    if ((d->kernel_variant == 2 || d->kernel_variant == 3) && !streamable)
+        { g_sel_err = "psgla_tv_step: shape not supported by the streaming kernel"; return -1; }
+    a.p2p = d->kernel_variant == 3 ? 1 : 0;
+    // small-batch tile kernel: forced (variant 4) or, in auto mode, when all tiles fit in one round
+    // on the CUs (a row stream would be mostly pipeline fill: strong scaling's 64/N chains per GPU)
+    a.tile_r = 0;
+    if (d->kernel_variant == 4 || d->kernel_variant == 0) {
+        const int P = d->B * d->C;
+        int bh = 0, nb = 0;
+        const int wg = (a.ldw == a.W) ? tile_geometry(P, d->H, d->W, d->n_tv, 3, &bh, &nb) : 0;
+        if (d->kernel_variant == 4 && wg == 0) { g_sel_err = "psgla_tv_step: shape not supported by the tile kernel"; return -1; }
+        if (wg > 0 && (d->kernel_variant == 4 || (long long)P * nb <= device_cus())) {
+            a.tile_r = 3;
+            a.band_h = bh;
+            a.nbands = nb;
+            a.nsegs = 1;
+            a.tiles = nb;
+            a.stream = 0;
+        }
+    }
+    if (!a.stream && a.tile_r == 0 && a.ldw != a.W) { g_sel_err = "psgla_tv_step: a row pitch ldw != W needs the streaming kernel"; return -1; }
+    a.split_wgs = 0;
+    a.st_nsegs = 1;
+    if (a.stream) {
+        a.st_halo = d->n_tv;
+        a.st_nsegs = stream_segments(a.W, a.ldw, d->n_tv, &a.st_seg_w);
+        if (choose_split((long long)d->B * d->C * a.st_nsegs, d->H, d->n_tv, d->stream_wgs, &a.split_wgs)) {
+            g_sel_err = g_err;
+            return -1;
+        }
+    }
+    if (a.tile_r > 0) return 3;
+    if (a.stream) return a.p2p ? 2 : 1;
     return 0;
 }
 
@@ -2194,27 +2766,25 @@ int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream) {
     a.n_inter = s->n_inter; a.nm = s->n_inter_mmse; a.coef = s->acc_coef;
     a.samples = s->samples; a.samples_cap = s->samples_cap;
     a.blocks = s->blocks; a.blocks2 = s->blocks2; a.blocks_cap = s->blocks_cap;
-    a.halo = d->n_tv;
-    tv_tiling(a);
-    const bool streamable = (a.ldw % 4 == 0) && d->n_tv >= 1 && d->n_tv <= SP_MAXST && d->H >= 2 &&
-                            stream_segments(a.W, a.ldw, d->n_tv, nullptr) > 0;
-    a.stream = streamable && d->kernel_variant != 1;
-    if (d->kernel_variant == 2 && !streamable) return fail(0, "psgla_tv_step: shape not supported by the streaming kernel");
-    if (!a.stream && a.ldw != a.W) return fail(0, "psgla_tv_step: a row pitch ldw != W needs the streaming kernel");
-    a.split_wgs = 0;
-    a.st_nsegs = 1;
-    if (a.stream) {
-        a.st_halo = d->n_tv;
-        a.st_nsegs = stream_segments(a.W, a.ldw, d->n_tv, &a.st_seg_w);
-        const int rc = choose_split((long long)d->B * d->C * a.st_nsegs, d->H, d->n_tv, d->stream_wgs,
-                                    &a.split_wgs);
-        if (rc) return rc;
-    }
+    if (select_step_kernel(d, a) < 0) return g_sel_err == g_err ? (int)hipErrorInvalidValue : fail(0, g_sel_err);
     hipStream_t st = (hipStream_t)stream;
     const int m = d->launch_mask;
     if (d->exact)
         return alpha1 ? launch_tv<true, FRONT_INPAINT, true>(a, st, m) : launch_tv<true, FRONT_INPAINT, false>(a, st, m);
     return alpha1 ? launch_tv<false, FRONT_INPAINT, true>(a, st, m) : launch_tv<false, FRONT_INPAINT, false>(a, st, m);
+}
+
+int psgla_tv_step_kernel(const PsglaTvStep* d) {
+    if (!d) return fail(0, "psgla_tv_step_kernel: null descriptor");
+    const int rc = check_tv_common(d->B, d->C, d->H, d->W, d->n_tv);
+    if (rc) return -1;
+    TvArgs a;
+    memset(&a, 0, sizeof(a));
+    a.B = d->B; a.C = d->C; a.H = d->H; a.W = d->W;
+    a.ldw = d->ldw > 0 ? d->ldw : d->W;
+    const int k = select_step_kernel(d, a);
+    if (k < 0 && g_sel_err != g_err) fail(0, g_sel_err);
+    return k;
 }
 
 int psgla_tv_prox(const PsglaTvProx* d, void* stream) {

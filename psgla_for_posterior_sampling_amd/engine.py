@@ -37,7 +37,7 @@ class FusedTvChains:
         # rows padded to a multiple of 4 columns so that every width runs on the streaming kernel
         # (psgla_kernels.hip: ldw); the padding columns are scratch and every result is a view
         # of the first W columns
-        self.ldw = Wd if (Wd % 4 == 0 or kernel_variant == "band") else (Wd + 3) // 4 * 4
+        self.ldw = Wd if (Wd % 4 == 0 or kernel_variant in ("band", "tile")) else (Wd + 3) // 4 * 4
         self.pshape = (B, C, H, self.ldw)
         self.device = dev
         self.alpha = float(alpha)
@@ -88,7 +88,7 @@ class FusedTvChains:
         d.fresh = self.work.fresh.data_ptr()
         d.norms = self.work.norms.data_ptr()
         d.arrive = self.work.arrive.data_ptr()
-        d.kernel_variant = {"auto": 0, "band": 1, "stream": 2}[kernel_variant]
+        d.kernel_variant = {"auto": 0, "band": 1, "stream": 2, "p2p": 3, "tile": 4}[kernel_variant]
         d.stream_wgs = int(stream_wgs)
         self.desc = d
         self.sched_struct = self.sched.struct(True, 0)
@@ -165,12 +165,14 @@ class FusedTvChains:
 
     @property
     def main_kernel(self) -> str:
-        """Name of the kernel psgla_tv_step dispatches for this shape (psgla_kernels.hip:
-        streaming when the row pitch is a multiple of 4 -- always, the engine pads rows --,
-        1 <= n_tv <= 10 and H >= 2, unless the band kernel is forced)."""
-        d = self.desc
-        streamable = d.ldw % 4 == 0 and 1 <= d.n_tv <= 10 and d.H >= 2
-        return "tv_stream_kernel" if streamable and d.kernel_variant != 1 else "tv_main_kernel"
+        """Name of the kernel psgla_tv_step dispatches for this shape (the library's own choice,
+        psgla_tv_step_kernel: the small-batch tile kernel when its tiles fit on the CUs at once, else
+        the row stream for W % 4 == 0 rows -- always, the engine pads rows --, 1 <= n_tv <= 10,
+        H >= 2; the band kernel otherwise or when forced)."""
+        k = N.lib().psgla_tv_step_kernel(ctypes.byref(self.desc))
+        if k < 0:
+            raise RuntimeError(N.lib().psgla_last_error().decode())
+        return ("tv_main_kernel", "tv_stream_kernel", "tv_stream_kernel", "tv_tile_kernel")[k]
 
     def launch_main_only(self, n: int = 1):
         """Launch only the fused tile kernel n times for the CURRENT step (idempotent: it reads

@@ -635,3 +635,98 @@ def test_stream_segmented_early_stop_exact_vs_oracle():
         np.testing.assert_array_equal(eng.samples()[:, b].cpu().numpy(), np.stack([t.numpy() for t in Xl]))
         np.testing.assert_array_equal(eng.u2_state[b].cpu().numpy(), tv.u2.numpy()[0])
     assert fired, "test needs the early stop to fire"
+
+
+# ------------------------------------------------------------------------------ P2P pipeline
+@pytest.mark.parametrize("exact,H,W,alpha,stream_wgs,tol,B", [
+    (True, 48, 64, 1.0, 0, 1e-5, 3), (True, 48, 64, 1.0, 7, 1e-5, 3), (True, 48, 64, 1.0, -1, 1e-5, 3),
+    (False, 48, 64, 1.0, 11, 1e-5, 3), (True, 70, 300, 1.0, 0, 1e-5, 2), (True, 37, 29, 0.6, 5, 1e-5, 3),
+    (True, 40, 52, 1.0, 0, 3e-2, 2), (False, 256, 256, 1.0, 0, 1e-5, 16)])
+def test_p2p_pipeline_equals_barrier_pipeline(exact, H, W, alpha, stream_wgs, tol, B):
+    """The stream kernel with point-to-point LDS progress waits (kernel_variant "p2p") computes exactly
+    what the barrier-synchronised pipeline computes (itself bit-identical to the oracle above): same
+    samples, block means, TV state, for row splits, column segments (W > 256, padded rows), alpha != 1,
+    early stops (tol 3e-2) and a full-size batch; no progress wait ever timed out (arrive[1] == 0)."""
+    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    g = torch.Generator().manual_seed(8)
+    x = torch.rand((1, 3, H, W), generator=g)
+    dg, y, init, mask2d = orc.inpainting_problem(x, seed_ip=1)
+    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
+    outs = []
+    for variant in ("stream", "p2p"):
+        eng = FusedTvChains(init.expand(B, -1, -1, -1).contiguous().to(DEV), y.to(DEV),
+                            mask2d.to(torch.uint8).to(DEV), c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
+                            alpha=alpha, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10, tol=tol),
+                            seed=3, n_iter=24, n_inter=5, n_inter_mmse=4, exact=exact, kernel_variant=variant,
+                            stream_wgs=stream_wgs)
+        eng.run(24, graph_steps=8)
+        torch.cuda.synchronize()
+        assert int(eng.work.arrive[1].item()) == 0, "a P2P progress wait timed out"
+        bm, bm2 = eng.blocks()
+        outs.append((eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+# ------------------------------------------------------------------------------ small-batch tile kernel
+@pytest.mark.parametrize("B,H,W,alpha,tol,n_tv", [(3, 48, 64, 1.0, 1e-5, 10), (2, 100, 64, 1.0, 1e-5, 10),
+                                                  (2, 77, 40, 0.6, 1e-5, 10), (2, 40, 52, 1.0, 3e-2, 10),
+                                                  (2, 90, 256, 1.0, 1e-5, 3), (1, 30, 20, 1.0, 1e-5, 14)])
+def test_tile_kernel_exact_vs_oracle(B, H, W, alpha, tol, n_tv):
+    """The small-batch tile kernel (one 48-row tile per workgroup, n_tv halo rows at band cuts, inline
+    finalisation) in exact mode: samples, block means and TV state bit-identical to the CPU oracle for
+    band cuts, narrow images (idle lanes), alpha != 1, deepinv's early stop and n_tv > 10."""
+    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    g = torch.Generator().manual_seed(9)
+    x = torch.rand((1, 3, H, W), generator=g)
+    dg, y, init, mask2d = orc.inpainting_problem(x, seed_ip=2)
+    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
+    n_iter = 14
+    eng = FusedTvChains(init.expand(B, -1, -1, -1).contiguous().to(DEV), y.to(DEV), mask2d.to(torch.uint8).to(DEV),
+                        c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)), alpha=alpha,
+                        ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=n_tv, tol=tol), seed=6,
+                        n_iter=n_iter, n_inter=3, n_inter_mmse=2, chain0=4, exact=True, kernel_variant="tile")
+    assert eng.main_kernel == "tv_tile_kernel"
+    eng.run(n_iter, graph_steps=6)
+    torch.cuda.synchronize()
+    bm, bm2 = eng.blocks()
+    for b in range(B):
+        tv = orc.TVDenoiser(n_it_max=n_tv, tol=tol)
+        Xl, Ml, M2l = orc.psgla(init, dg, tv, torch.tensor(alpha), torch.tensor(10.0), sig_float=10 / 255.0,
+                                delta=(10 / 255.0) ** 2, n_iter=n_iter, n_inter=3, n_inter_mmse=2, seed=6, chain=4 + b)
+        np.testing.assert_array_equal(eng.samples()[:, b].cpu().numpy(), np.stack([t.numpy() for t in Xl]))
+        np.testing.assert_array_equal(bm[:, b].cpu().numpy(), np.stack([t.numpy() for t in Ml]))
+        np.testing.assert_array_equal(bm2[:, b].cpu().numpy(), np.stack([t.numpy() for t in M2l]))
+        np.testing.assert_array_equal(eng.x2_state[b].cpu().numpy(), tv.x2.numpy()[0])
+        np.testing.assert_array_equal(eng.u2_state[b].cpu().numpy(), tv.u2.numpy()[0])
+
+
+@pytest.mark.parametrize("B", [8, 16])
+def test_tile_kernel_equals_stream_kernel_full_size(B):
+    """Strong-scaling batch sizes at the benched image size (3 x 256 x 256): the tile kernel and the
+    row-streaming kernel give bit-identical chains in both arithmetic modes (the same per-element
+    operations; the exact stream kernel is bit-identical to the oracle)."""
+    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    g = torch.Generator(device=DEV).manual_seed(1234)
+    xs = torch.rand((B, 3, 256, 256), generator=g, device=DEV)
+    gen = torch.Generator(device=DEV).manual_seed(0)
+    mask2d = (torch.rand((256, 256), generator=gen, device=DEV) > 0.5).to(torch.uint8)
+    y = mask2d.float() * xs + torch.normal(torch.zeros_like(xs), std=(1 / 255.0) * torch.ones_like(xs),
+                                           generator=gen)
+    init = (mask2d.float() * y + (1 - mask2d.float()) * 0.5).contiguous()
+    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
+    for exact in (True, False):
+        outs = []
+        for variant in ("stream", "tile"):
+            eng = FusedTvChains(init, y.contiguous(), mask2d, c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
+                                alpha=1.0, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10), seed=0,
+                                n_iter=30, n_inter=10, n_inter_mmse=10, exact=exact, kernel_variant=variant)
+            eng.run(30, graph_steps=10)
+            torch.cuda.synchronize()
+            bm, bm2 = eng.blocks()
+            outs.append((eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone()))
+        for a, b in zip(*outs):
+            assert torch.equal(a, b), f"exact={exact}"
