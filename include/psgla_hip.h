@@ -208,6 +208,19 @@ int pnpula_update(const float* X, const float* gp, const float* gd, float* Xout,
                   int32_t B, int64_t E, uint64_t seed, int32_t chain0, const PsglaSchedule* s,
                   void* stream);
 
+/* PnP-ULA step with the DNN prior fused ("V-ULA"): replaces, in one pass over the chain state,
+ *   gp = (alpha * (D - X)) / s2             DenoiserPrior, sampling_images.py:156-157 (D = D(X, s1))
+ *   gd = ((-m) * (X - y)) / sigma2          sampling_images.py:295, when gd == NULL (inpainting;
+ *                                           y / mask as psgla_inpaint_grad), else the given gd
+ *                                           (deblurring: psgla_blur_grad's output)
+ *   the update of pnpula_update (restoration_algorithms.py:104-115) and its accumulators.
+ * Same fp32 operations in the same order as those three steps (bit-identical); 32 B/elem at
+ * inpainting (read X, D, y, mean, sq; write X', mean, sq).  X, D, Xout: (B, C, H, W). */
+int pnpula_prior_update(const float* X, const float* D, float alpha, float s2, const float* gd, const float* y,
+                        int64_t y_chain_stride, const uint8_t* mask, int64_t mask_chain_stride, float sigma2,
+                        float* Xout, float delta, float lambd, float brw, float c_min, float c_max, float* mean,
+                        float* sq, int32_t B, int32_t C, int32_t H, int32_t W, uint64_t seed, int32_t chain0,
+                        const PsglaSchedule* s, void* stream);
 /* g = ((-m) * (X - y)) / sigma2, mask (H,W) u8 per chain (sampling_images.py:295) */
 int psgla_inpaint_grad(const float* X, const float* y, int64_t y_chain_stride, const uint8_t* mask,
                        int64_t mask_chain_stride, float* g, int32_t B, int32_t C, int32_t H,

@@ -75,6 +75,9 @@ _SIGNATURES = {
                                              ctypes.POINTER(PsglaSchedule), c_vp]),
     "pnpula_update": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_f, c_f, c_f, c_f, c_f, c_vp, c_vp, c_i32, c_i64,
                               c_u64, c_i32, ctypes.POINTER(PsglaSchedule), c_vp]),
+    "pnpula_prior_update": (c_i32, [c_vp, c_vp, c_f, c_f, c_vp, c_vp, c_i64, c_vp, c_i64, c_f, c_vp, c_f, c_f, c_f,
+                                    c_f, c_f, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_u64, c_i32,
+                                    ctypes.POINTER(PsglaSchedule), c_vp]),
     "psgla_inpaint_grad": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i32, c_i32, c_i32, c_i32, c_f,
                                    c_vp]),
     "psgla_blur_grad": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32,

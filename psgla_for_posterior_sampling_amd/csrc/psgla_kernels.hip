@@ -111,11 +111,31 @@ __device__ __forceinline__ float f4get(const float4& v, int k) {
     return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w));
 }
 
+// Sum over the 64 lanes, returned in every lane.  DPP within each row of 16 lanes (xor 1, xor 2 by
+// quad_perm, then row rotations by 4 and 8: every lane holds its row's sum), then the four row sums
+// read out by v_readlane: pure VALU, no LDS round trips (a __shfl_xor tree is six dependent
+// ds_bpermute's, ~0.5 us per tracked TV iteration on the tile kernel's critical path).
+#ifdef PSGLA_WAVESUM_SHFL
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
     return v;
 }
+#else
+#define PSGLA_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), (ctrl), 0xF, 0xF, false))
+__device__ __forceinline__ float wave_sum(float v) {
+    v += PSGLA_DPP(v, 0xB1);      // quad_perm [1,0,3,2]: lane ^ 1
+    v += PSGLA_DPP(v, 0x4E);      // quad_perm [2,3,0,1]: lane ^ 2
+    v += PSGLA_DPP(v, 0x124);     // row_ror:4
+    v += PSGLA_DPP(v, 0x128);     // row_ror:8
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return (r0 + r1) + (r2 + r3);
+}
+#undef PSGLA_DPP
+#endif
 
 // Block-mean accumulator + sample storage for one element (restoration_algorithms.py:240-271).
 // idx = chain*E + e within the batch; BE = B*E (slot stride of samples/blocks).
@@ -632,6 +652,18 @@ __device__ __forceinline__ void st_nt(float* p, const float4& v) {
     // s_nop: the compiler does not see this store, so it cannot pad the store-data hazard
     // (a VALU write of the data VGPRs right after a >8-byte store) -- the asm does
     asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
+}
+
+// Output store of the tile kernel: write-through (sc1) by default -- all its workgroups finish together
+// and each then releases (writes back) its XCD's dirty L2 lines before the arrival count, which
+// write-through stores leave clean; -DPSGLA_TILE_ST_NT: nt stores as the stream kernel.
+__device__ __forceinline__ void st_tile(float* p, const float4& v) {
+#if defined(PSGLA_TILE_ST_NT)
+    st_nt(p, v);
+#else
+    const v4f x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
+#endif
 }
 
 // Diagnostic build (-DPSGLA_STAMPS): every wave accumulates the cycles it spends working
@@ -1760,19 +1792,27 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
 
     // ---- 4. inner TV iterations (deepinv 0.2.1 TVDenoiser, the stream kernel's arithmetic)
     const bool lastlane = gj0 + CPL == W;              // holds column W-1: no forward difference there
+    // Trapezoid: the core rows need iteration j (1-based) only on rows [r0 - (n_it - j), r1 + (n_it - j))
+    // for the dual and one row more below for the primal (the dual of a row reads the next row's z);
+    // a wave none of whose rows is needed skips the phase (its stale rows feed only unneeded rows).
+    const int wr0 = e0 + w * R, wr1 = wr0 + R;
     for (int it = 0; it < n_it; ++it) {
         const bool trk = track && it >= trk_lo(a) && it <= trk_hi(a);
         float sd = 0.f, sn = 0.f;
+        const int span = n_it - 1 - it;
+        const bool act_p = wr1 > r0 - span && wr0 < r1 + span + 1;
+        const bool act_d = wr1 > r0 - span && wr0 < r1 + span;
         // primal: x = prox_tau_fx(x2 - tau nabla^T u2, Y); z = 2x - x2; x2 += rho (x - x2)
         const float4 up = (w > 0) ? sh.urow[w - 1][lane] : zero4;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
+            if (!act_p) break;
             const float u1l = __int_as_float(
                 __builtin_amdgcn_update_dpp(0, __float_as_int(u1[r][CPL - 1]), 0x138 /* wave_shr:1 */, 0xF, 0xF, true));
-            const bool top = gi[r] == 0;
 #pragma unroll
             for (int k = 0; k < CPL; ++k) {
-                const float pu = top ? 0.f : ((r > 0) ? u0[r - 1][k] : f4get(up, k));
+                // the row above: 0 above the tile's first row (the plane's top row or an artificial halo edge)
+                const float pu = (r > 0) ? u0[r - 1][k] : f4get(up, k);
                 const float u1left = (k > 0) ? u1[r][k - 1] : u1l;
                 const float tt = ((pu - u0[r][k]) - u1[r][k]) + u1left;
                 const float xo = x2[r][k];
@@ -1804,7 +1844,7 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
                 x2[r][k] = xn;
             }
         }
-        sh.zrow[w][lane] = make_float4(z[0][0], z[0][1], z[0][2], z[0][3]);
+        if (act_p) sh.zrow[w][lane] = make_float4(z[0][0], z[0][1], z[0][2], z[0][3]);
         if (trk) {
             sd = wave_sum(sd);
             sn = wave_sum(sn);
@@ -1816,6 +1856,7 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
         const float4 dn = (w < TV_NW - 1) ? sh.zrow[w + 1][lane] : zero4;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
+            if (!act_d) break;
             const float zr3 = __int_as_float(
                 __builtin_amdgcn_update_dpp(0, __float_as_int(z[r][0]), 0x130 /* wave_shl:1 */, 0xF, 0xF, true));
             const bool down = gi[r] < H - 1;
@@ -1845,7 +1886,7 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
                 }
             }
         }
-        sh.urow[w][lane] = make_float4(u0[R - 1][0], u0[R - 1][1], u0[R - 1][2], u0[R - 1][3]);
+        if (act_d) sh.urow[w][lane] = make_float4(u0[R - 1][0], u0[R - 1][1], u0[R - 1][2], u0[R - 1][3]);
         __syncthreads();
     }
     // ---- 5. rel_err partial sums -> the chain's norms (one fp64 atomic per iteration and workgroup)
@@ -1869,11 +1910,11 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
         for (int k = 0; k < CPL; ++k)
             Xo[k] = ALPHA1 ? x2[r][k] : (1.0f - a.alpha) * yv[r][k] + a.alpha * x2[r][k];
         const float4 X4 = make_float4(Xo[0], Xo[1], Xo[2], Xo[3]);
-        st_nt(a.x[par_out] + base, X4);
+        st_tile(a.x[par_out] + base, X4);
         float* u2o = a.u2[par_out] + 2 * base;
-        st_nt(u2o, make_float4(u0[r][0], u1[r][0], u0[r][1], u1[r][1]));
-        st_nt(u2o + 4, make_float4(u0[r][2], u1[r][2], u0[r][3], u1[r][3]));
-        if (!ALPHA1) st_nt(a.x2[par_out] + base, make_float4(x2[r][0], x2[r][1], x2[r][2], x2[r][3]));
+        st_tile(u2o, make_float4(u0[r][0], u1[r][0], u0[r][1], u1[r][1]));
+        st_tile(u2o + 4, make_float4(u0[r][2], u1[r][2], u0[r][3], u1[r][3]));
+        if (!ALPHA1) st_tile(a.x2[par_out] + base, make_float4(x2[r][0], x2[r][1], x2[r][2], x2[r][3]));
         if (si.acc) {
             float4 bm = zero4, bq = zero4;
             if (need_prev) {
@@ -1896,14 +1937,14 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
             const float4 M4 = make_float4(m[0], m[1], m[2], m[3]);
             const float4 Q4 = make_float4(q[0], q[1], q[2], q[3]);
             if (si.blockend) {
-                st_nt(a.blocks + (size_t)si.blk * BE + base, M4);
-                st_nt(a.blocks2 + (size_t)si.blk * BE + base, Q4);
+                st_tile(a.blocks + (size_t)si.blk * BE + base, M4);
+                st_tile(a.blocks2 + (size_t)si.blk * BE + base, Q4);
             } else if (si.liveout) {
-                st_nt(a.mean[par_out] + base, M4);
-                st_nt(a.sq[par_out] + base, Q4);
+                st_tile(a.mean[par_out] + base, M4);
+                st_tile(a.sq[par_out] + base, Q4);
             }
         }
-        if (si.sample) st_nt(a.samples + (size_t)si.sidx * BE + base, X4);
+        if (si.sample) st_tile(a.samples + (size_t)si.sidx * BE + base, X4);
     }
 }
 
@@ -2425,6 +2466,72 @@ __global__ void pnpula_update_kernel(const float* X, const float* gp, const floa
     }
 }
 
+// PnP-ULA step with the DNN prior fused ("V-ULA", restoration_algorithms.py:104-115 with the prior of
+// sampling_images.py:156-157): gp = (alpha (D - X)) / s2 from the denoiser output D = D(X, s1), the
+// inpainting data term gd = ((-m)(X - y)) / sigma2 computed in place (gd == nullptr) or a given gd
+// (deblurring: the stencil kernel's output), the projection, the update, the noise and the
+// accumulators in one pass -- read X, D, y, mean, sq (+ the shared mask), write X', mean, sq: 32 B/elem.
+// The same fp32 operations, in the same order, as DenoiserPrior's torch ops + psgla_inpaint_grad +
+// pnpula_update.  grid: (quads of a chain, chain); quads are chain-linear (the noise quads).
+__global__ void pnpula_prior_update_kernel(const float* X, const float* D, float alpha, float s2, const float* gd,
+                                           const float* y, long long y_cs, const uint8_t* mask, long long m_cs,
+                                           float sigma2, float* Xo, float delta, float lambd, float brw, float cmin,
+                                           float cmax, int B, long long HW, long long E, float* mean, float* sq,
+                                           unsigned long long seed, int chain0, AccArgs s) {
+    const long long step = read_step(s.d_step, s.off);
+    const long long Q = (E + 3) >> 2;
+    const size_t BE = (size_t)B * E;
+    const int b = blockIdx.y;
+    const bool vec = (E & 3) == 0 && (HW & 3) == 0;
+    const AccStep st = acc_step(s, step, mean);
+    const float* yp = y ? y + (size_t)b * y_cs : nullptr;
+    const uint8_t* mp = mask ? mask + (size_t)b * m_cs : nullptr;
+    auto upd = [&](float x, float d, float gdv, float zz) {
+        const float gpv = (alpha * (d - x)) / s2;
+        const float out = (x > cmin) ? x : cmin;
+        const float proj = (out < cmax) ? out : cmax;
+        const float gpi = (gpv - (x - proj) / lambd) + gdv;
+        return (x + delta * gpi) + brw * zz;
+    };
+    for (long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x; q < Q;
+         q += (long long)gridDim.x * blockDim.x) {
+        float z[4];
+        normal_quad(seed, (uint32_t)(chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)q, z);
+        const size_t i0 = (size_t)b * E + (size_t)(q << 2);
+        if (vec) {
+            const float4 x = ld4(X + i0), d = ld4(D + i0);
+            float g[4];
+            if (gd) {
+                const float4 g4 = ld4(gd + i0);
+                g[0] = g4.x; g[1] = g4.y; g[2] = g4.z; g[3] = g4.w;
+            } else {
+                const long long e = q << 2;
+                const float4 yy = ld4(yp + e);
+                const uint32_t m = *reinterpret_cast<const uint32_t*>(mp + (e % HW));
+                g[0] = (-(float)(m & 0xFFu) * (x.x - yy.x)) / sigma2;
+                g[1] = (-(float)((m >> 8) & 0xFFu) * (x.y - yy.y)) / sigma2;
+                g[2] = (-(float)((m >> 16) & 0xFFu) * (x.z - yy.z)) / sigma2;
+                g[3] = (-(float)(m >> 24) * (x.w - yy.w)) / sigma2;
+            }
+            const float4 xn = make_float4(upd(x.x, d.x, g[0], z[0]), upd(x.y, d.y, g[1], z[1]),
+                                          upd(x.z, d.z, g[2], z[2]), upd(x.w, d.w, g[3], z[3]));
+            st4(Xo + i0, xn.x, xn.y, xn.z, xn.w);
+            acc_quad(s, st, i0, BE, xn, mean, sq);
+        } else {
+            for (int j = 0; j < 4; ++j) {
+                const long long e = (q << 2) + j;
+                if (e >= E) break;
+                const size_t i = i0 + j;
+                const float x = X[i];
+                const float gdv = gd ? gd[i] : (-(float)mp[e % HW] * (x - yp[e])) / sigma2;
+                const float xn = upd(x, D[i], gdv, z[j]);
+                Xo[i] = xn;
+                acc_elem(s, step, i, BE, xn, mean, sq);
+            }
+        }
+    }
+}
+
 // DnCNN layer epilogue (denoisers.py DnCNN, deepinv's conv -> bias -> ReLU): y = relu(y + bias[c]) in
 // place, one pass instead of PyTorch's bias add and ReLU passes over a 1 GB activation tensor at 64
 // chains.  NHWC (hw == 0: c = e % C, C % 4 == 0) or NCHW (c = (e / hw) % C, hw % 4 == 0).  ReLU as
@@ -2891,6 +2998,23 @@ int pnpula_update(const float* X, const float* gp, const float* gd, float* Xout,
                        gd, Xout, delta, lambd, brw, c_min, c_max, B, (long long)E, mean, sq,
                        (unsigned long long)seed, chain0, make_acc(s));
     return launch_check("pnpula_update");
+}
+
+int pnpula_prior_update(const float* X, const float* D, float alpha, float s2, const float* gd, const float* y,
+                        int64_t y_chain_stride, const uint8_t* mask, int64_t mask_chain_stride, float sigma2, float* Xout,
+                        float delta, float lambd, float brw, float c_min, float c_max, float* mean, float* sq, int32_t B,
+                        int32_t C, int32_t H, int32_t W, uint64_t seed, int32_t chain0, const PsglaSchedule* s,
+                        void* stream) {
+    if (!X || !D || !Xout || !s || B <= 0 || C <= 0 || H <= 0 || W <= 0) return fail(0, "pnpula_prior_update: bad arguments");
+    if (!gd && (!y || !mask)) return fail(0, "pnpula_prior_update: needs gd or the inpainting y / mask");
+    if (s->n_inter_mmse >= 0 && (!mean || !sq || !s->acc_coef)) return fail(0, "pnpula_prior_update: accumulators missing");
+    if (B > 65535) return fail(0, "pnpula_prior_update: more than 65535 chains in one launch");
+    const long long HW = (long long)H * W, E = (long long)C * HW;
+    hipLaunchKernelGGL(pnpula_prior_update_kernel, dim3(grid_chain(E / 4 + 1, B), B), dim3(256), 0, (hipStream_t)stream,
+                       X, D, alpha, s2, gd, y, (long long)y_chain_stride, mask, (long long)mask_chain_stride, sigma2,
+                       Xout, delta, lambd, brw, c_min, c_max, B, HW, E, mean, sq, (unsigned long long)seed, chain0,
+                       make_acc(s));
+    return launch_check("pnpula_prior_update");
 }
 
 int psgla_inpaint_grad(const float* X, const float* y, int64_t y_chain_stride, const uint8_t* mask,

@@ -412,6 +412,15 @@ class UlaChains(_GraphRunner):
         self.sq = torch.zeros_like(X0)
         self.data_grad, self.prior_grad = data_grad, prior_grad
         self.delta, self.lambd, self.brw = float(delta), float(lambd), float(brw)
+        # V-ULA: a DenoiserPrior's arithmetic (alpha (D - x) / s2), the data term and the update in one
+        # HIP pass after the denoiser forward (the scalars read once here, outside any capture)
+        from .denoisers import DenoiserPrior
+        from .fidelity import BlurFidelity, InpaintingFidelity
+        self.fused = isinstance(prior_grad, DenoiserPrior) and isinstance(data_grad, (InpaintingFidelity, BlurFidelity))
+        if self.fused:
+            self.alpha_f = float(torch.as_tensor(prior_grad.alpha).float().item())
+            self.s2_f = float(torch.as_tensor(prior_grad.s2).float().item())
+            self.inpaint = isinstance(data_grad, InpaintingFidelity)
         self.c_min, self.c_max = float(c_min), float(c_max)
         self.seed, self.chain0 = int(seed), int(chain0)
         self.n_iter = int(n_iter)
@@ -423,10 +432,23 @@ class UlaChains(_GraphRunner):
 
     def _body(self):
         X, Xn = self.X[self.cur], self.X[1 - self.cur]
-        gp = self.prior_grad(X).contiguous().float()
-        gd = self.data_grad(X).contiguous().float()
-        K.pnpula_update(X, gp, gd, Xn, self.delta, self.lambd, self.brw, self.c_min, self.c_max, self.mean, self.sq,
-                        self.sched, 0, self.seed, self.chain0, use_device_step=True)
+        if self.fused:
+            p, f = self.prior_grad, self.data_grad
+            D = p.denoiser.forward(X, p.s1).contiguous().float()
+            if self.inpaint:
+                K.pnpula_prior_update(X, D, self.alpha_f, self.s2_f, Xn, self.delta, self.lambd, self.brw, self.c_min,
+                                      self.c_max, self.mean, self.sq, self.sched, 0, self.seed, self.chain0, y=f.y,
+                                      mask_u8=f.mask_u8, sigma2=f.sigma2, use_device_step=True)
+            else:
+                gd = f(X).contiguous().float()
+                K.pnpula_prior_update(X, D, self.alpha_f, self.s2_f, Xn, self.delta, self.lambd, self.brw, self.c_min,
+                                      self.c_max, self.mean, self.sq, self.sched, 0, self.seed, self.chain0, gd=gd,
+                                      use_device_step=True)
+        else:
+            gp = self.prior_grad(X).contiguous().float()
+            gd = self.data_grad(X).contiguous().float()
+            K.pnpula_update(X, gp, gd, Xn, self.delta, self.lambd, self.brw, self.c_min, self.c_max, self.mean,
+                            self.sq, self.sched, 0, self.seed, self.chain0, use_device_step=True)
         K.advance_step(self.sched.d_step)
         self.cur ^= 1
 

@@ -158,6 +158,25 @@ def pnpula_update(X, gp, gd, X_out, delta: float, lambd: float, brw: float, c_mi
     return X_out
 
 
+def pnpula_prior_update(X, D, alpha: float, s2: float, X_out, delta: float, lambd: float, brw: float, c_min: float,
+                        c_max: float, mean, sq, sched: Schedule, step: int, seed: int, chain0: int, *, gd=None, y=None,
+                        mask_u8=None, sigma2: float = 1.0, use_device_step: bool = False):
+    """PnP-ULA step with the DNN prior fused (V-ULA): gp = (alpha (D - X)) / s2, the inpainting data term
+    (y, mask_u8, sigma2) or a given gd, the update, noise and accumulators in one HIP pass."""
+    B, C, H, W = X.shape
+    s = sched.struct(use_device_step, step)
+    y_cs = 0 if (y is None or y.shape[0] == 1) else C * H * W
+    m_cs = 0 if (mask_u8 is None or mask_u8.dim() == 2 or mask_u8.shape[0] == 1) else H * W
+    N.check(N.lib().pnpula_prior_update(
+        _ptr(X, name="X"), _ptr(D, name="D"), float(alpha), float(s2), _ptr(gd, name="gd") if gd is not None else None,
+        _ptr(y, name="y") if y is not None else None, y_cs,
+        _ptr(mask_u8, torch.uint8, "mask") if mask_u8 is not None else None, m_cs, float(sigma2),
+        _ptr(X_out, name="Xout"), float(delta), float(lambd), float(brw), float(c_min), float(c_max),
+        _ptr(mean, name="mean"), _ptr(sq, name="sq"), B, C, H, W, seed & (2 ** 64 - 1), int(chain0), ctypes.byref(s),
+        _stream()), "pnpula_prior_update")
+    return X_out
+
+
 def bias_act_(y: torch.Tensor, bias: torch.Tensor, relu: bool = True) -> torch.Tensor:
     """In place y = relu(y + bias[c]) (or y + bias[c]) for an (N, C, H, W) conv output in NHWC
     (channels_last) or NCHW memory; the DnCNN layer epilogue (one HBM pass instead of two)."""

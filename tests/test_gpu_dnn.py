@@ -113,12 +113,16 @@ def test_denoiser_chains_vs_oracle():
     assert rel(M, Mr) < REL_TOL_MEAN
 
 
-def test_ula_chains_graph_equals_step_loop():
+@pytest.mark.parametrize("H,W,deblur", [(32, 48, False), (37, 45, False), (32, 48, True)])
+def test_ula_chains_graph_equals_step_loop(H, W, deblur):
     """pnpula with a DenoiserPrior (DRUNet/DnCNN prior of sampling_images.py:156-157): UlaChains
-    (hipGraph replay) == the step-by-step loop with the same prior as an opaque closure."""
+    (hipGraph replay, the prior's arithmetic + data term + update fused in one V-ULA pass,
+    pnpula_prior_update) == the step-by-step loop with the prior as an opaque closure (DenoiserPrior's
+    torch ops, the data-term kernel, pnpula_update), bit for bit: inpainting on 4-aligned and odd planes,
+    deblurring (the stencil's gd fed to the fused pass)."""
     from psgla_for_posterior_sampling_amd import restoration_algorithms as RA
     from psgla_for_posterior_sampling_amd.denoisers import DenoiserPrior
-    dg, init = problem()
+    dg, init = problem(H=H, W=W, deblur=deblur)
     den = small_dncnn(seed=2).to(DEV)
     s1 = 5 / 255.0
     prior = DenoiserPrior(den, s1, torch.tensor(1.0, device=DEV), torch.tensor(s1 ** 2, device=DEV))
