@@ -1,14 +1,16 @@
 #!/bin/bash
 # Round profile of the bench command on the GPU box: kernel-trace stats of the driver's bench command
 # and the PMC passes (one counter group per run, MI355X_MICROARCH.md's rocprofv3 rules) summarised by
-# tools/pmc_summary.py.  Usage: tools/profile_round.sh ROUND COMMIT [extra bench args]
-# (writes gpurun_out/prof_ROUND*; copy the summaries into profiles/)
+# tools/pmc_summary.py.  Usage: tools/profile_round.sh TAG COMMIT KERNEL CHAINS [extra bench args]
+# (writes gpurun_out/prof_TAG*; copy the summaries into profiles/)
 set -e
 cd "$(dirname "$0")/.."
 R=${1:-r02}
 COMMIT=${2:-unknown}
-shift 2 || true
-EXTRA="$*"
+KERNEL=${3:-tv_stream_kernel}
+CHAINS=${4:-64}
+shift 4 || true
+EXTRA="--batch $CHAINS $*"
 export TMPDIR=/tmp
 O=gpurun_out/prof_$R
 mkdir -p $O
@@ -23,5 +25,5 @@ for c in "FETCH_SIZE" "WRITE_SIZE" \
   timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $O/pmc$i -o p -- \
     python3 bench.py --steps 40 --warmup 4 --warmup-seconds 0.3 --no-cpu --kernel-iters 5 $EXTRA > $O/bench_pmc$i.json
 done
-python3 tools/pmc_summary.py --round $R --kernel tv_stream_kernel --commit $COMMIT --command "python3 $CMD" \
-  --out $O/pmc_tv_stream.json $O/pmc1 $O/pmc2 $O/pmc3 $O/pmc4
+python3 tools/pmc_summary.py --round $R --kernel $KERNEL --chains $CHAINS --commit $COMMIT --command "python3 $CMD" \
+  --out $O/pmc.json $O/pmc1 $O/pmc2 $O/pmc3 $O/pmc4
