@@ -51,7 +51,9 @@ sys.path.insert(0, REPO)
 
 METRIC = "Langevin steps/sec (3×256×256, batch=64) at 1/2/4/8 GPU; HBM GB/s vs roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PMC_PROFILE = os.path.join("profiles", "r02_pmc_tv_stream.json")
+# committed PMC summaries (tools/profile_round.sh + tools/pmc_summary.py) by dominant kernel
+PMC_PROFILES = {"tv_stream_kernel": os.path.join("profiles", "r02b_pmc_tv_stream.json"),
+                "tv_tile_kernel": os.path.join("profiles", "r02b_pmc_tv_tile.json")}
 
 
 def parse():
@@ -74,7 +76,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the batch-1 CPU leg")
     p.add_argument("--cpu-b64-steps", type=int, default=10, help="timed steps of the batch-64 CPU leg (0: skip)")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--pmc-json", default=os.path.join(REPO, PMC_PROFILE))
+    p.add_argument("--pmc-json", default=None, help="PMC summary to report as roofline.traffic (default: the "
+                   "committed profile of the dispatched kernel, when it was measured on this workload)")
     return p.parse_args()
 
 
@@ -275,13 +278,15 @@ def main():
     psnr_sum, n_chains = reduce_psnr(blocks, xs, world)
 
     traffic, traffic_info = None, None
-    if os.path.exists(args.pmc_json):
+    pmc_json = args.pmc_json or os.path.join(REPO, PMC_PROFILES.get(eng.main_kernel, "none"))
+    if os.path.exists(pmc_json):
         try:
-            pj = json.load(open(args.pmc_json))
-            if (pj.get("workload", {}).get("chains_per_gpu") in (None, B) and pj.get("exact", False) == args.exact
+            pj = json.load(open(pmc_json))
+            if (pj.get("kernel") == eng.main_kernel and pj.get("workload", {}).get("chains_per_gpu") in (None, B)
+                    and pj.get("exact", False) == args.exact
                     and args.tv_iters == 10 and (H, W) == (256, 256)):
                 traffic = pj.get("hbm_bytes_per_launch")
-                traffic_info = {"traffic_source": os.path.relpath(args.pmc_json, REPO),
+                traffic_info = {"traffic_source": os.path.relpath(pmc_json, REPO),
                                 "traffic_commit": pj.get("commit"),
                                 "traffic_note": "rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE), not measured in this run"}
         except Exception:
