@@ -168,11 +168,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU over RCCL ("nccl"); PSGLA_DIST_BACKEND=gloo rehearses the multi-rank path on a
+    # box with fewer GPUs than ranks (ranks then share devices: plumbing only, the timings mean nothing)
+    backend = os.environ.get("PSGLA_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    local_dev = local % max(ndev, 1)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    dev = torch.device(f"cuda:{local}")
+        torch.cuda.set_device(local_dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_dev}"))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device(f"cuda:{local_dev}")
     torch.cuda.set_device(dev)
 
     from psgla_for_posterior_sampling_amd import hip_ops as K
@@ -254,7 +262,7 @@ def main():
     live_kern_ms = ev0.elapsed_time(ev1) / steps     # kernel + its launch boundary, in the timed region
     if world > 1:
         import torch.distributed as dist
-        t = torch.tensor([dt], device=dev)
+        t = torch.tensor([dt], device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
@@ -317,6 +325,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic (U[0,1) images per chain, reference mask/observation recipe)",
             "config": {"workload": "psgla+TV inpainting 50% (BASELINE configs[1]), n_it_max=10",
+                       "dist_backend": backend if world > 1 else None,
                        "global_batch": total_chains, "chains_per_gpu": B, "image": [C, H, W],
                        "parallelism": f"chains{world}", "graph_steps": gs,
                        "kernel_mode": "exact" if args.exact else "fast",

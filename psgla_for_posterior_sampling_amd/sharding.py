@@ -44,6 +44,8 @@ def reduce_psnr(blocks: torch.Tensor | None, gt: torch.Tensor, world: int):
         vals = torch.stack([p.sum(), torch.tensor(float(p.numel()), dtype=torch.float64, device=gt.device)])
     if world > 1:
         import torch.distributed as dist
+        if dist.get_backend() == "gloo":        # gloo: host tensors (CPU tests, single-GPU rehearsals)
+            vals = vals.cpu()
         dist.all_reduce(vals, op=dist.ReduceOp.SUM)
     s, n = vals.tolist()
     return s, int(round(n)) if not math.isnan(n) else 0
@@ -55,7 +57,8 @@ def gather_chains(local: torch.Tensor, total: int, world: int):
         return local
     import torch.distributed as dist
     per = -(-total // world)
-    buf = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    dev = "cpu" if dist.get_backend() == "gloo" else local.device
+    buf = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=dev)
     buf[: local.shape[0]] = local
     out = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(out, buf)
@@ -63,4 +66,4 @@ def gather_chains(local: torch.Tensor, total: int, world: int):
     for r in range(world):
         a, b = chain_range(total, world, r)
         parts.append(out[r][: b - a])
-    return torch.cat(parts, dim=0)
+    return torch.cat(parts, dim=0).to(local.device)

@@ -73,3 +73,26 @@ def test_cli_pnpula_inpainting_random_drunet(tmp_path):
     recs = SI.main(argv)
     assert len(recs) == 1 and np.isfinite(recs[0]["PSNR_y"])
     assert len(recs[0]["PSNR_sample"]) == 1000
+
+
+def test_bench_multirank_rehearsal():
+    """bench.py's multi-rank path (torch.distributed.run, strong split of the 64 chains, barriers, max over
+    ranks, the PSNR all_reduce) with 2 ranks on this box's one GPU over gloo (PSGLA_DIST_BACKEND): every
+    chain's samples do not depend on the split, so the mean MMSE PSNR equals the 1-rank run's."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    base = ["bench.py", "--steps", "20", "--warmup", "5", "--no-cpu", "--kernel-iters", "3", "--warmup-seconds", "0"]
+    env = dict(os.environ, PSGLA_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", "29533"] + base + ["--gpus", "2"],
+                         cwd=repo, env=env, capture_output=True, text=True, timeout=240)
+    assert two.returncode == 0, two.stderr[-2000:]
+    d2 = json.loads([l for l in two.stdout.splitlines() if l.startswith("{")][-1])
+    one = subprocess.run([sys.executable] + base, cwd=repo, capture_output=True, text=True, timeout=240)
+    assert one.returncode == 0, one.stderr[-2000:]
+    d1 = json.loads([l for l in one.stdout.splitlines() if l.startswith("{")][-1])
+    assert d2["n_gpus"] == 2 and d2["config"]["chains_per_gpu"] == 32 and d2["config"]["global_batch"] == 64
+    assert d2["scaling"] == "strong" and d2["value"] > 0
+    assert abs(d2["mmse_psnr_mean_db"] - d1["mmse_psnr_mean_db"]) < 1e-9
