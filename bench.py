@@ -72,7 +72,7 @@ def parse():
     p.add_argument("--kernel-iters", type=int, default=50)
     p.add_argument("--tv-iters", type=int, default=10, help="TV n_it_max (analysis only; the workload is 10)")
     p.add_argument("--stream-wgs", type=int, default=0, help="stream kernel work split (0 auto, -1 per plane)")
-    p.add_argument("--variant", choices=["auto", "band", "stream", "p2p", "tile"], default="auto", help="fused TV kernel (analysis)")
+    p.add_argument("--variant", choices=["auto", "band", "stream", "p2p", "tile", "wave"], default="auto", help="fused TV kernel (analysis)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the batch-1 CPU leg")
     p.add_argument("--cpu-b64-steps", type=int, default=10, help="timed steps of the batch-64 CPU leg (0: skip)")
     p.add_argument("--no-cpu", action="store_true")

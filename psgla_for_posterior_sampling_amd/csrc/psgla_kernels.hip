@@ -95,6 +95,8 @@ struct TvArgs {
     int fin_inline;                 // stream kernel: 1 = the last workgroup finalises the step
     int p2p;                        // stream kernel: 1 = point-to-point LDS progress waits instead of barriers
     int tile_r;                     // > 0: small-batch tile kernel with tile_r rows per wave (one tile per workgroup)
+    int wave;                       // 1: per-wave pipeline kernel
+    int wv_slots, wv_base, wv_extra, wv_whole;   // its row ranges (wave_item)
     unsigned long long* stamps;     // diagnostic build only (PSGLA_STAMPS): per-wave work/wait cycles
 };
 
@@ -606,6 +608,7 @@ struct StreamShared {
 
 typedef __attribute__((address_space(1))) const void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
+typedef float v4f_t __attribute__((ext_vector_type(4)));
 
 // 16 B (4 B) per lane from global memory straight into LDS; lane i lands at dst + 16 i (4 i).
 // Issued as inline asm: the compiler does not track these loads, so it cannot insert a
@@ -620,6 +623,26 @@ __device__ __forceinline__ void glds4(const void* src, void* dst) {
     const unsigned off = (unsigned)(size_t)(lptr_t)dst;
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off"
                  :: "v"(src), "s"(off) : "memory", "m0");
+}
+// SGPR-base forms (per-wave pipeline kernel): global_* with a wave-uniform 64-bit base in SGPRs (saddr) and
+// a 32-bit per-lane byte offset in one VGPR -- no 64-bit per-lane address stays live across the row loop
+// (a spilled one is reloaded behind a compiler vmcnt(0) that serialises the hand-placed DMAs).  No
+// immediate offsets (an LDS-DMA's would also move its LDS destination).
+// 16 B (4 B) per lane straight into LDS: lane i lands at dst + 16 i (4 i)
+__device__ __forceinline__ void sglds16(const void* sbase, uint32_t voff, void* dst) {
+    const unsigned m = (unsigned)(size_t)(lptr_t)dst;
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                 :: "v"(voff), "s"(sbase), "s"(m) : "memory", "m0");
+}
+__device__ __forceinline__ void sglds4(const void* sbase, uint32_t voff, void* dst) {
+    const unsigned m = (unsigned)(size_t)(lptr_t)dst;
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1"
+                 :: "v"(voff), "s"(sbase), "s"(m) : "memory", "m0");
+}
+// 16-B streaming (nt) store; s_nop: the store-data hazard the compiler cannot see
+__device__ __forceinline__ void sgst16(void* sbase, uint32_t voff, const float4& v) {
+    const v4f_t x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 1" :: "v"(voff), "v"(x), "s"(sbase) : "memory");
 }
 // Workgroup barrier that only drains LDS (lgkmcnt): LDS-DMA loads stay in flight across it
 // (a __syncthreads() fence would wait vmcnt(0) while a global_load_lds is pending).
@@ -2018,6 +2041,527 @@ __global__ void __launch_bounds__(TV_THREADS) tv_tile_kernel(const TvArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Per-wave pipelines: the fused step with no LDS ring and no barrier ("wave kernel",
+// kernel_variant 5).
+//
+// The stream kernel hands every row from one inner TV iteration (a wave) to the next through LDS
+// rings, one workgroup barrier per row (~34 ds_write_b128 + ~50 ds_read_b128 per row, 16 waves
+// released in lock-step): latency-bound at ~0.41 of the HBM roofline.  Here ONE wave runs the whole
+// pipeline of its own row range -- front (LDS-DMA loads, noise, data term), all n inner iterations,
+// back (relaxation, accumulators, stores) -- skewed by one row per iteration: at step t iteration k
+// runs its primal on stream row t - k + 1 and its dual on row t - k, so each input is either this
+// step's output of iteration k - 1 or the iteration's own state from the previous step.  That state
+// (u2^{k-1} and z^k of one row, x2^k of the same row: 16 VGPRs per iteration and lane) stays in
+// registers; LDS holds only the wave's own Y rows (prox anchor of rows t - n .. t) and its LDS-DMA
+// staging.  Nothing crosses waves.  8 waves per CU (2 per SIMD, <= 256 VGPRs) run independent
+// contiguous row ranges of the concatenated planes (build_rowmap), n halo rows where a range is cut
+// inside a plane; iteration k computes only the rows the core's dependency cone needs (trapezoid).
+// The per-element arithmetic is the stream kernel's in both modes.  W <= 256, W % 4 == 0, ldw == W.
+// ---------------------------------------------------------------------------------------
+constexpr int WV_NW = 8;                  // waves (= row ranges) per workgroup
+constexpr int WV_THREADS = WV_NW * WAVE;
+constexpr int WV_YS = SP_MAXST + 1;       // Y ring slots: stream rows t - n .. t
+constexpr int WV_MAXC = 8;                // chains per workgroup whose rel-err sums meet in LDS first
+
+struct WaveLds {
+    float4 y[WV_YS][WAVE];                // Y rows by stream row % WV_YS
+    float4 fx[WAVE], fy[WAVE], fu0[WAVE], fu1[WAVE], fxs[WAVE];   // front staging: X, y, u2, x2
+    uint32_t fm[WAVE];                    // front staging: mask (4 columns per lane)
+    float4 bm[WAVE], bq[WAVE];            // back staging: mean / sq of the back's row
+    float red[SP_MAXSEG][SP_MAXST][2];    // rel-err partial sums per (segment, inner iteration)
+};
+struct WaveShared {
+    WaveLds w[WV_NW];
+    int s_stop[MAXG];
+    double wred[WV_MAXC][SP_MAXST][2];
+    int s_flag, s_item;
+};
+
+// Primal update of one row (deepinv: x = prox_tau_fx(x2 - tau nabla^T u2, Y); z = 2x - x2;
+// x2 += rho (x - x2)), the stream kernel's stage_phase_a arithmetic.  dx: (x - x2_prev) in fast mode
+// (the rel-err term), unused in exact mode.
+template <bool EXACT>
+__device__ __forceinline__ void wv_primal(const TvArgs& a, const float (&xo)[CPL], const float (&u0)[CPL],
+                                          const float (&u1)[CPL], const float (&yy)[CPL], const float (&pu0)[CPL],
+                                          float (&z)[CPL], float (&xn)[CPL], float (&dx)[CPL]) {
+    // u1 of the column left of this lane's first column (lane-1's last); 0 at lane 0
+    const float u1l = __int_as_float(
+        __builtin_amdgcn_update_dpp(0, __float_as_int(u1[CPL - 1]), 0x138 /* wave_shr:1 */, 0xF, 0xF, true));
+#pragma unroll
+    for (int kk = 0; kk < CPL; ++kk) {
+        const float u1left = kk > 0 ? u1[kk - 1] : u1l;
+        const float tt = ((pu0[kk] - u0[kk]) - u1[kk]) + u1left;
+        const float x = xo[kk];
+        if (EXACT) {
+            const float xv = ((x - a.tau * tt) + a.tau * yy[kk]) / a.opt;
+            z[kk] = 2.0f * xv - x;
+            xn[kk] = x + a.rho * (xv - x);
+            dx[kk] = 0.f;
+        } else {
+            const float xv = __builtin_fmaf(a.tau, yy[kk] - tt, x) * a.inv_opt;
+            z[kk] = __builtin_fmaf(2.0f, xv, -x);
+            dx[kk] = xv - x;
+            xn[kk] = __builtin_fmaf(a.rho, dx[kk], x);
+        }
+    }
+}
+
+// Dual update of one row (deepinv: u = prox_sigma_g_conj(u2 + sigma nabla z, ths); u2 += rho (u - u2)),
+// the stream kernel's stage_phase_b arithmetic.  DN: the row has a row below (zd = its z).
+template <bool EXACT, bool DN>
+__device__ __forceinline__ void wv_dual(const TvArgs& a, const float (&u0)[CPL], const float (&u1)[CPL],
+                                        const float (&zc)[CPL], const float (&zd)[CPL], bool lastlane,
+                                        float (&un0)[CPL], float (&un1)[CPL]) {
+    // z of the column right of this lane's last column (lane+1's first)
+    const float zr3 = __int_as_float(
+        __builtin_amdgcn_update_dpp(0, __float_as_int(zc[0]), 0x130 /* wave_shl:1 */, 0xF, 0xF, true));
+#pragma unroll
+    for (int kk = 0; kk < CPL; ++kk) {
+        const float z = zc[kk];
+        const float zr = kk < CPL - 1 ? zc[kk + 1] : zr3;
+        const float g0 = DN ? (zd[kk] - z) : 0.0f;
+        float g1 = zr - z;
+        if (kk == CPL - 1) g1 = lastlane ? 0.0f : g1;     // the image's last column (W % 4 == 0)
+        const float uo0 = u0[kk], uo1 = u1[kk];
+        if (EXACT) {
+            const float v0 = uo0 + a.sig_tv * g0;
+            const float v1 = uo1 + a.sig_tv * g1;
+            const float nrm = sqrtf(v0 * v0 + v1 * v1) / a.ths;
+            const float dd = fmaxf(nrm, 1.0f);
+            un0[kk] = uo0 + a.rho * (v0 / dd - uo0);
+            un1[kk] = uo1 + a.rho * (v1 / dd - uo1);
+        } else {
+            const float v0 = __builtin_fmaf(a.sig_tv, g0, uo0);
+            const float v1 = __builtin_fmaf(a.sig_tv, g1, uo1);
+            const float s2 = __builtin_fmaf(v0, v0, v1 * v1);
+            const float f = fminf(1.0f, a.ths * __builtin_amdgcn_rsqf(s2));
+            un0[kk] = __builtin_fmaf(a.rho, __builtin_fmaf(v0, f, -uo0), uo0);
+            un1[kk] = __builtin_fmaf(a.rho, __builtin_fmaf(v1, f, -uo1), uo1);
+        }
+    }
+}
+
+// Row range of one wave: core rows [H part / parts, H (part + 1) / parts) of `plane` and the h halo rows
+// around them inside the plane (a RowMap with one segment; ranges never cross a plane boundary).
+// Q = 0: empty part.
+__device__ __forceinline__ void part_rowmap(int H, int h, int plane, int part, int parts, RowMap& m) {
+    const int c0 = H * part / parts, c1 = H * (part + 1) / parts;
+    const int lo = max(0, c0 - h), hi = min(H, c1 + h);
+    m.ns = 1;
+    m.Q = c1 > c0 ? hi - lo : 0;
+    m.htop = c0 - lo;
+    m.hbot = hi - c1;
+    m.q1 = m.q2 = m.q3 = m.Q;
+    m.pl0 = plane; m.pl1 = m.pl2 = m.pl3 = 0;
+    m.lo0 = lo; m.lo1 = m.lo2 = m.lo3 = 0;
+}
+
+// Range slot g of a launch -> its plane and part.  wv_whole == 0: plane p is cut into wv_base parts
+// (wv_base + 1 for the first wv_extra planes), one per slot; wv_whole == 1 (more planes than slots):
+// slot g takes the whole planes g, g + slots, ... (item i of the slot).  false: nothing (more).
+__device__ __forceinline__ bool wave_item(const TvArgs& a, int g, int i, int& plane, int& part, int& parts) {
+    const int P = a.B * a.C;
+    if (a.wv_whole) {
+        plane = g + i * a.wv_slots;
+        part = 0;
+        parts = 1;
+        return plane < P;
+    }
+    if (i > 0) return false;
+    const int big = a.wv_base + 1, nbig = a.wv_extra * big;
+    if (g < nbig) {
+        plane = g / big; part = g - plane * big; parts = big;
+    } else {
+        const int g2 = g - nbig;
+        plane = a.wv_extra + g2 / a.wv_base; part = g2 - (plane - a.wv_extra) * a.wv_base; parts = a.wv_base;
+    }
+    return plane < P;
+}
+
+template <int M> struct WvMode { static constexpr int v = M; };
+
+// One wave's pass over the rows of `rm` (one plane, rows lo0 .. lo0 + Q - 1) with n inner iterations.
+// track: deepinv's rel-err terms of the core rows are added to the chain's sums (the workgroup's LDS
+// accumulator wred for chains c0g .. c0g + WV_MAXC - 1, else the global ones).
+//
+// Schedule: at step t the front loads / makes row t; iteration k runs its primal on row p = t - k + 1
+// (inputs x2^{k-1}, u2^{k-1} of row p handed on from iteration k - 1 within the step, the row above's
+// u2^{k-1}[..., 0] from its own state) and its dual on row p - 1 (its own state: u2^{k-1}, z^k of row
+// p - 1, and the new z of row p); the back finishes row t - n.  Iteration k runs the rows
+// [max(0, lo_k - 1), hi_k] with lo_k = max(0, qc0 - (n - k)), hi_k = min(Q, qc1 + n - k) (the core's
+// dependency cone, one row more at each end); where the stream ends at the plane's bottom the row
+// p = Q is a virtual primal (z of row Q := z of row Q - 1, so the dual of the last row sees no vertical
+// difference, as deepinv's nabla).  The state starts at zero, so the first primal of a plane-top stream
+// sees u2 = 0 above, as deepinv's nabla^T.
+template <bool EXACT, bool ALPHA1>
+__device__ __forceinline__ void wave_pass(const TvArgs& a, WaveLds& L, const RowMap& rm, const int n,
+                                          const bool track, const long long step, const bool fresh,
+                                          double (*wred)[SP_MAXST][2], const int c0g) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int H = a.H, W = a.W, C = a.C;
+    const size_t HW = (size_t)H * W;
+    const size_t E = (size_t)C * HW;
+    const size_t BE = (size_t)a.B * E;
+    const int par_in = (int)(step & 1), par_out = (int)((step + 1) & 1);
+    const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int Q = rm.Q;
+    const int qc0 = rm.htop, qc1 = Q - rm.hbot;          // core stream rows
+    const bool bottom = rm.hbot == 0;                     // the stream ends at the plane's last row
+    const int plane = rm.pl0, r0 = rm.lo0;                // stream row q = plane row r0 + q
+    const int chain = plane / C, cc = plane - chain * C;
+    const int gj0 = CPL * lane;
+    const bool lane_ok = gj0 < W;
+    const int gjc = min(gj0, W - CPL);                     // DMA source column (every lane in bounds)
+    const bool lastlane = gj0 + CPL == W;
+    const StepInfo si = step_info(a, step, a.mean[par_out]);
+    const bool need_prev = si.acc && !si.first;
+    const size_t pbase = (size_t)plane * HW + (size_t)r0 * W;          // stream row 0 of the state buffers
+    const size_t ybase = (size_t)chain * a.y_cs + (size_t)cc * HW + (size_t)r0 * W;
+    const size_t mbase = (size_t)chain * a.m_cs + (size_t)r0 * W;
+    const uint32_t vo_c = (uint32_t)gjc * 4u;              // byte offsets in a row: DMA lanes (clamped) / stores
+    const uint32_t vo_s = (uint32_t)gj0 * 4u;
+    // vector-memory stores per core row of the back (lane 0 always holds a real column: every store issues)
+    const int nst = 3 + (ALPHA1 ? 0 : 1) + ((si.acc && (si.blockend || si.liveout)) ? 2 : 0) + (si.sample ? 1 : 0);
+
+    auto lo_k = [&](int k) { return max(0, qc0 - (n - k)); };
+    auto hi_k = [&](int k) { return min(Q, qc1 + (n - k)); };
+    // iteration k runs its primal at steps [tb_k, te_k] (rows max(0, lo_k - 1) .. hi_k, and the virtual
+    // row Q below a plane-bottom stream); tb_k and te_k do not decrease with k, so the iterations active
+    // at a step are an interval [kmin, kmax]
+    auto tb_k = [&](int k) { return max(0, lo_k(k) - 1) + k - 1; };
+    auto te_k = [&](int k) { return (bottom ? hi_k(k) : min(hi_k(k), Q - 1)) + k - 1; };
+    const int t_beg = max(0, lo_k(1) - 1);                // front rows [t_beg, t_fend)
+    const int t_fend = min(Q, hi_k(1) + 1);
+    const int nsteps = qc1 + n;                            // the back finishes core row qc1 - 1
+    // steady steps (n == SP_MAXST only): every iteration on a real row, front active: [t_st0, t_st1)
+    const int t_st0 = n == SP_MAXST ? max(t_beg, tb_k(n)) : nsteps;
+    const int t_st1 = n == SP_MAXST ? min(t_fend, min(nsteps, min(Q, hi_k(n) + 1) + n - 1)) : nsteps;
+    // bases of this stream's row 0 (accumulators: the live means or the block slot; the sample slot)
+    float* const xo_g = a.x[par_out] + pbase;
+    float* const u2o_g = a.u2[par_out] + 2 * pbase;
+    float* const x2o_g = ALPHA1 ? nullptr : a.x2[par_out] + pbase;
+    float* const accm_g = !si.acc ? nullptr : (si.blockend ? a.blocks + (size_t)si.blk * BE + pbase : (si.liveout ? a.mean[par_out] + pbase : nullptr));
+    float* const accq_g = !si.acc ? nullptr : (si.blockend ? a.blocks2 + (size_t)si.blk * BE + pbase : (si.liveout ? a.sq[par_out] + pbase : nullptr));
+    float* const smp_g = si.sample ? a.samples + (size_t)si.sidx * BE + pbase : nullptr;
+    const float* const xi_g = a.x[par_in] + pbase;
+    const float* const u2i_g = a.u2[par_in] + 2 * pbase;
+    const float* const x2i_g = ALPHA1 ? nullptr : a.x2[par_in] + pbase;
+    const float* const yi_g = a.yobs + ybase;
+    const uint8_t* const mi_g = a.mask + mbase;
+    const float* const mean_in = a.mean[par_in] + pbase;
+    const float* const sq_in = a.sq[par_in] + pbase;
+
+    auto front_dma = [&](int q) {
+        const size_t o = (size_t)q * W;
+        sglds16(xi_g + o, vo_c, &L.fx[0]);
+        sglds16(yi_g + o, vo_c, &L.fy[0]);
+        sglds16(u2i_g + 2 * o, 2u * vo_c, &L.fu0[0]);
+        sglds16(u2i_g + 2 * o + 4, 2u * vo_c, &L.fu1[0]);
+        sglds4(mi_g + o, (uint32_t)gjc, &L.fm[0]);
+        if (!ALPHA1) sglds16(x2i_g + o, vo_c, &L.fxs[0]);
+    };
+    auto back_dma = [&](int q) {
+        const size_t o = (size_t)q * W;
+        sglds16(mean_in + o, vo_c, &L.bm[0]);
+        sglds16(sq_in + o, vo_c, &L.bq[0]);
+    };
+
+    // iteration k's state (index k - 1): u2^{k-1} and z^k of the row of its last primal, x2^k of it
+    float Su0[SP_MAXST][CPL], Su1[SP_MAXST][CPL], Sz[SP_MAXST][CPL], Sx[SP_MAXST][CPL];
+#pragma unroll
+    for (int k = 0; k < SP_MAXST; ++k) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) { Su0[k][c] = 0.f; Su1[k][c] = 0.f; Sz[k][c] = 0.f; Sx[k][c] = 0.f; }
+    }
+    // rel-err sums: only iterations it = k - 1 in [2, n - 2] are tracked, i.e. k in [3, 9] (index k - 3)
+    constexpr int NTRK = SP_MAXST - 3;
+    float tsd[NTRK], tsn[NTRK];
+#pragma unroll
+    for (int i = 0; i < NTRK; ++i) { tsd[i] = 0.f; tsn[i] = 0.f; }
+
+    int nyoung = 0;                          // vector-memory ops issued after the front DMA of the next row
+    // one step: MODE 0 = steady (every iteration on a real row, front active), 1 = general (fill / drain)
+    auto do_step = [&](const int t, auto mode) {
+        constexpr int MODE = decltype(mode)::v;
+        int kmin = 1, kmax = SP_MAXST;
+        if (MODE == 1) {
+            kmin = n + 1;
+            kmax = 0;
+            for (int k = n; k >= 1; --k) {
+                if (te_k(k) >= t) kmin = k;
+                if (kmax == 0 && tb_k(k) <= t) kmax = k;
+            }
+        }
+        const int bq_row = t - n;            // the back's row
+        const bool bk = bq_row >= qc0 && bq_row < qc1;
+        // ---------------- front: row t -> Y(t), x2^0(t), u2^0(t) ----------------
+        float xin[CPL], ui0[CPL], ui1[CPL], yin[CPL];
+        if (MODE == 0 || t < t_fend) {
+            const size_t e = ((size_t)cc * H + (r0 + t)) * W + gj0;  // element index in the chain's C*H*W image
+            float Zn[CPL];
+            normal_quad(a.seed, (uint32_t)(a.chain0 + chain), (uint32_t)step, TAG_LANGEVIN, (uint32_t)(e >> 2), Zn);
+            wait_vm_n(nyoung);               // row t's staging landed (issued one step ago)
+            const float4 fX = L.fx[lane], fYo = L.fy[lane], fU0 = L.fu0[lane], fU1 = L.fu1[lane];
+            const float4 fXS = ALPHA1 ? zero4 : L.fxs[lane];
+            const uint32_t fM = L.fm[lane];
+            const float X[CPL] = {fX.x, fX.y, fX.z, fX.w};
+            const float yo[CPL] = {fYo.x, fYo.y, fYo.z, fYo.w};
+            const float mk[CPL] = {(float)(fM & 0xFFu), (float)((fM >> 8) & 0xFFu), (float)((fM >> 16) & 0xFFu),
+                                   (float)(fM >> 24)};
+            const float xs[CPL] = {fXS.x, fXS.y, fXS.z, fXS.w};
+            const float us0[CPL] = {fU0.x, fU0.z, fU1.x, fU1.z};
+            const float us1[CPL] = {fU0.y, fU0.w, fU1.y, fU1.w};
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                float Y;
+                if (EXACT) {
+                    const float g = (-mk[c] * (X[c] - yo[c])) / a.sigma2;
+                    Y = (X[c] + a.c1 * g) + a.c2 * Zn[c];
+                } else {
+                    const float g = (mk[c] * (yo[c] - X[c])) * a.inv_sigma2;
+                    Y = __builtin_fmaf(a.c2, Zn[c], __builtin_fmaf(a.c1, g, X[c]));
+                }
+                yin[c] = lane_ok ? Y : 0.f;
+                xin[c] = lane_ok ? (fresh ? Y : (ALPHA1 ? X[c] : xs[c])) : 0.f;
+                ui0[c] = (lane_ok && !fresh) ? us0[c] : 0.f;
+                ui1[c] = (lane_ok && !fresh) ? us1[c] : 0.f;
+            }
+            L.y[t % WV_YS][lane] = make_float4(yin[0], yin[1], yin[2], yin[3]);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // staging read before it is re-targeted
+            nyoung = 0;
+            if (t + 1 < t_fend) front_dma(t + 1);
+            if (bk && need_prev) { back_dma(bq_row); nyoung = 2; }
+        } else {
+            if (bk && need_prev) back_dma(bq_row);
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) { xin[c] = 0.f; ui0[c] = 0.f; ui1[c] = 0.f; yin[c] = 0.f; }
+        }
+        // ---------------- inner iterations k = 1..n ----------------
+#pragma unroll
+        for (int k = 1; k <= SP_MAXST; ++k) {
+            const int p = t - k + 1;
+            if (MODE == 0 || (k >= kmin && k <= kmax)) {
+                float yk[CPL];
+                if (k == 1) {
+#pragma unroll
+                    for (int c = 0; c < CPL; ++c) yk[c] = yin[c];
+                } else {
+                    const float4 Y4 = L.y[p % WV_YS][lane];
+                    yk[0] = Y4.x; yk[1] = Y4.y; yk[2] = Y4.z; yk[3] = Y4.w;
+                }
+                float zn[CPL], xn[CPL], dx[CPL];
+                if (MODE == 1 && p == Q) {
+                    // virtual row below the plane: the dual of row Q - 1 gets z(Q) - z(Q - 1) = 0
+#pragma unroll
+                    for (int c = 0; c < CPL; ++c) { zn[c] = Sz[k - 1][c]; xn[c] = 0.f; dx[c] = 0.f; }
+                } else {
+                    wv_primal<EXACT>(a, xin, ui0, ui1, yk, Su0[k - 1], zn, xn, dx);
+                    if (k >= 3 && k <= NTRK + 2 && track && (k - 1) <= n - 2 && p >= qc0 && p < qc1) {
+#pragma unroll
+                        for (int c = 0; c < CPL; ++c) {
+                            if (EXACT) {
+                                const float d = xin[c] - xn[c];
+                                const float q = xn[c] + 1e-12f;
+                                tsd[k - 3] = __builtin_fmaf(d, d, tsd[k - 3]);
+                                tsn[k - 3] = __builtin_fmaf(q, q, tsn[k - 3]);
+                            } else {
+                                tsd[k - 3] = __builtin_fmaf(dx[c], dx[c], tsd[k - 3]);
+                                tsn[k - 3] = __builtin_fmaf(xn[c], xn[c], tsn[k - 3]);
+                            }
+                        }
+                    }
+                }
+                float un0[CPL], un1[CPL];
+                wv_dual<EXACT, true>(a, Su0[k - 1], Su1[k - 1], Sz[k - 1], zn, lastlane, un0, un1);
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) {
+                    const float xo = Sx[k - 1][c];
+                    Sx[k - 1][c] = xn[c];
+                    Sz[k - 1][c] = zn[c];
+                    Su0[k - 1][c] = ui0[c];
+                    Su1[k - 1][c] = ui1[c];
+                    xin[c] = xo;
+                    ui0[c] = un0[c];
+                    ui1[c] = un1[c];
+                }
+            }
+        }
+        // ---------------- back: row t - n (x2^n = xin, u2^n = ui0 / ui1) ----------------
+        if (bk) {
+            float Xo[CPL];
+            if (ALPHA1) {
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) Xo[c] = xin[c];
+            } else {
+                const float4 Y4 = L.y[bq_row % WV_YS][lane];
+                const float yy[CPL] = {Y4.x, Y4.y, Y4.z, Y4.w};
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) Xo[c] = (1.0f - a.alpha) * yy[c] + a.alpha * xin[c];
+            }
+            float4 M4 = zero4, Q4 = zero4;
+            if (si.acc) {
+                float4 bm = zero4, bq = zero4;
+                if (need_prev) {
+                    wait_vm0();              // mean / sq of this row (issued at the step's front)
+                    bm = L.bm[lane];
+                    bq = L.bq[lane];
+                }
+                const float ms[CPL] = {bm.x, bm.y, bm.z, bm.w};
+                const float qs[CPL] = {bq.x, bq.y, bq.z, bq.w};
+                float m[CPL], qq[CPL];
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) {
+                    if (si.first) {
+                        m[c] = si.cb * Xo[c];
+                        qq[c] = si.cb * (Xo[c] * Xo[c]);
+                    } else {
+                        m[c] = si.ca * ms[c] + si.cb * Xo[c];
+                        qq[c] = si.ca * qs[c] + si.cb * (Xo[c] * Xo[c]);
+                    }
+                }
+                M4 = make_float4(m[0], m[1], m[2], m[3]);
+                Q4 = make_float4(qq[0], qq[1], qq[2], qq[3]);
+                // the back staging read before the next step's DMA re-targets it
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+            const size_t o = (size_t)bq_row * W;
+            const float4 X4 = make_float4(Xo[0], Xo[1], Xo[2], Xo[3]);
+            if (lane_ok) {
+                sgst16(xo_g + o, vo_s, X4);
+                sgst16(u2o_g + 2 * o, 2u * vo_s, make_float4(ui0[0], ui1[0], ui0[1], ui1[1]));
+                sgst16(u2o_g + 2 * o + 4, 2u * vo_s, make_float4(ui0[2], ui1[2], ui0[3], ui1[3]));
+                if (!ALPHA1) sgst16(x2o_g + o, vo_s, make_float4(xin[0], xin[1], xin[2], xin[3]));
+                if (accm_g) {
+                    sgst16(accm_g + o, vo_s, M4);
+                    sgst16(accq_g + o, vo_s, Q4);
+                }
+                if (smp_g) sgst16(smp_g + o, vo_s, X4);
+            }
+            nyoung += nst;
+        }
+    };
+
+    if (t_beg < t_fend) front_dma(t_beg);
+    int t = t_beg;
+    for (; t < min(t_st0, nsteps); ++t) do_step(t, WvMode<1>());
+    for (; t < t_st1; ++t) do_step(t, WvMode<0>());
+    for (; t < nsteps; ++t) do_step(t, WvMode<1>());
+    if (track) {
+        // the chain's rel-err sums of this range: iteration k's terms -> wred / norms (fp64)
+#pragma unroll
+        for (int k = 3; k <= NTRK + 2; ++k) {
+            if ((k - 1) <= n - 2) {
+                float d = wave_sum(lane_ok ? tsd[k - 3] : 0.f);
+                const float q = wave_sum(lane_ok ? tsn[k - 3] : 0.f);
+                if (!EXACT) d *= a.rho * a.rho;     // fast sums hold (x - x2_prev)^2
+                if (lane == 0) {
+                    const int it = k - 1;
+                    if (chain - c0g >= 0 && chain - c0g < WV_MAXC) {
+                        atomicAdd(&wred[chain - c0g][it][0], (double)d);
+                        atomicAdd(&wred[chain - c0g][it][1], (double)q);
+                    } else {
+                        atomicAdd(&a.norms[((size_t)chain * a.n_tv + it) * 2], (double)d);
+                        atomicAdd(&a.norms[((size_t)chain * a.n_tv + it) * 2 + 1], (double)q);
+                    }
+                }
+            }
+        }
+    }
+}
+
+template <bool EXACT, bool ALPHA1>
+__global__ void __launch_bounds__(WV_THREADS) tv_wave_kernel(const TvArgs a) {
+    __shared__ WaveShared sh;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long long step = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
+    const bool fresh = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
+    const int C = a.C;
+    const int g = (int)blockIdx.x * WV_NW + w;
+    // first chain of the workgroup's ranges: chains c0g .. c0g + WV_MAXC - 1 meet in LDS first
+    int c0g = 0;
+    {
+        int pl, pt, pts;
+        if (wave_item(a, (int)blockIdx.x * WV_NW, 0, pl, pt, pts)) c0g = pl / C;
+    }
+    for (int i = threadIdx.x; i < WV_MAXC * SP_MAXST * 2; i += blockDim.x) (&sh.wred[0][0][0])[i] = 0.0;
+    __syncthreads();
+    if (g < a.wv_slots) {
+        int pl, pt, pts;
+        for (int i = 0; wave_item(a, g, i, pl, pt, pts); ++i) {
+            RowMap rm;
+            part_rowmap(a.H, a.n_tv, pl, pt, pts, rm);
+            if (rm.Q > 0) wave_pass<EXACT, ALPHA1>(a, sh.w[w], rm, a.n_tv, true, step, fresh, sh.wred, c0g);
+        }
+    }
+    if (!a.fin_inline) return;            // main-pass-only launch (kernel timing): no side effects
+    __syncthreads();
+    for (int i = threadIdx.x; i < WV_MAXC * SP_MAXST; i += blockDim.x) {
+        const int gg = i / SP_MAXST, it = i - gg * SP_MAXST, ch = c0g + gg;
+        if (ch < a.B && it >= 2 && it <= a.n_tv - 2) {
+            const double d = sh.wred[gg][it][0], q = sh.wred[gg][it][1];
+            if (d != 0.0 || q != 0.0) {
+                atomicAdd(&a.norms[((size_t)ch * a.n_tv + it) * 2], d);
+                atomicAdd(&a.norms[((size_t)ch * a.n_tv + it) * 2 + 1], q);
+            }
+        }
+    }
+    // ---- step finalisation by the last workgroup to arrive (as tv_stream_kernel) ----
+    wait_vm0();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const int old = __hip_atomic_fetch_add(a.arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sh.s_flag = (old == (int)gridDim.x - 1) ? 1 : 0;
+        if (sh.s_flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    wait_vm0();
+    __syncthreads();
+    if (!sh.s_flag) return;
+    const int G = a.B;
+    for (int gg = threadIdx.x; gg < G; gg += blockDim.x) sh.s_stop[gg] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < G * SP_MAXST; i += blockDim.x) {
+        const int gg = i / SP_MAXST, t = i - gg * SP_MAXST;
+        if (t >= 2 && t <= a.n_tv - 2) {
+            const double nd = a.norms[((size_t)gg * a.n_tv + t) * 2];
+            const double nn = a.norms[((size_t)gg * a.n_tv + t) * 2 + 1];
+            const float rel = (float)sqrt(nd) / (float)sqrt(nn);
+            if (rel < a.tol) atomicOr(&sh.s_stop[gg], 1 << t);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) sh.s_item = 0;
+    __syncthreads();
+    for (int gg = threadIdx.x; gg < G; gg += blockDim.x) {
+        const int m = sh.s_stop[gg];
+        sh.s_stop[gg] = m ? (__ffs(m) - 1) + 1 : a.n_tv;
+        if (m) sh.s_item = 1;                 // some chain stopped early (benign race: all write 1)
+    }
+    __syncthreads();
+    if (sh.s_item) {
+        // rare: every plane of a stopped chain again with the stopped iteration count, split over the
+        // workgroup's waves (the step's inputs are intact: ping-pong state)
+        const int P = a.B * C;
+        for (int pl = 0; pl < P; ++pl) {
+            const int nstop = __builtin_amdgcn_readfirstlane(sh.s_stop[pl / C]);
+            if (nstop < a.n_tv) {
+                RowMap pm;
+                part_rowmap(a.H, a.n_tv, pl, w, WV_NW, pm);
+                if (pm.Q > 0) wave_pass<EXACT, ALPHA1>(a, sh.w[w], pm, nstop, false, step, fresh, sh.wred, c0g);
+            }
+        }
+        wait_vm0();
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.B * a.n_tv * 2; i += blockDim.x) a.norms[i] = 0.0;
+    if (threadIdx.x == 0) {
+        *a.arrive = 0;
+        if (a.fresh_dev) *a.fresh_dev = 0;
+        if (a.advance_step && a.d_step) *a.d_step = *a.d_step + 1;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // Generic elementwise kernels (opaque closures; also the first / last steps of fused paths)
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ long long read_step(const long long* d, long long off) {
@@ -2707,6 +3251,30 @@ static int tile_geometry(int P, int H, int W, int h, int R, int* band_h, int* nb
     return ((P + 7) / 8) * 8 * nb;
 }
 
+// Row ranges of the per-wave pipeline kernel: one per wave slot (8 per CU).  P planes <= slots: plane p is
+// cut into base (+1 for the first `extra` planes) parts of >= 16 core rows each; more planes than slots:
+// whole planes, slot g taking planes g, g + slots, ...  Returns the number of slots (a multiple of WV_NW),
+// 0 if the shape does not fit (W > 256, W % 4, ldw != W, n_tv outside [1, 10], H < 2).
+static int wave_geometry(long long P, int H, int W, int ldw, int n_tv, TvArgs* a) {
+    if (W > TV_COLS || (W & 3) || ldw != W || n_tv < 1 || n_tv > SP_MAXST || H < 2) return 0;
+    const long long slots = (long long)device_cus() * WV_NW;
+    int whole = 0, base = 1, extra = 0;
+    long long used;
+    if (P >= slots) {
+        whole = 1;
+        used = slots;
+    } else {
+        const long long maxparts = H / 16 > 1 ? H / 16 : 1;
+        base = (int)(slots / P);
+        extra = (int)(slots % P);
+        if (base >= maxparts) { base = (int)maxparts; extra = 0; }
+        used = P * base + extra;
+    }
+    used = (used + WV_NW - 1) / WV_NW * WV_NW;
+    if (a) { a->wv_slots = (int)used; a->wv_base = base; a->wv_extra = extra; a->wv_whole = whole; }
+    return (int)used;
+}
+
 // Column segments of the streaming kernel: equal core widths (multiples of 4) cut from the image
 // width W; segment s's wave covers columns [f0, f0 + 256) with f0 = (cc0 - h) & ~3 (cc0 = s * seg_w),
 // which must reach cc1 + h for interior cuts (the TV dependency cone) and the row pitch L at the
@@ -2735,6 +3303,12 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
     const int P = a.B * a.C;
     if (mask == 0) mask = 3;
     if (mask & 1) {
+        if (FRONT == FRONT_INPAINT && a.wave) {
+            TvArgs s = a;
+            s.fin_inline = (mask & 2) ? 1 : 0;
+            hipLaunchKernelGGL((tv_wave_kernel<EXACT, ALPHA1>), dim3(s.wv_slots / WV_NW), dim3(WV_THREADS), 0, st, s);
+            return launch_check("tv_wave_kernel");
+        }
         if (FRONT == FRONT_INPAINT && a.tile_r > 0) {
             TvArgs s = a;
             s.fin_inline = (mask & 2) ? 1 : 0;
@@ -2818,6 +3392,18 @@ static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
             a.tiles = nb;
             a.stream = 0;
         }
+    }
+    // per-wave pipeline kernel: forced (variant 5)
+    a.wave = 0;
+    if (d->kernel_variant == 5) {
+        if (wave_geometry((long long)d->B * d->C, d->H, d->W, a.ldw, d->n_tv, &a) == 0)
+            { g_sel_err = "psgla_tv_step: shape not supported by the wave kernel"; return -1; }
+        a.wave = 1;
+        a.split_wgs = 0;
+        a.st_nsegs = 1;
+        a.stream = 0;
+        a.tile_r = 0;
+        return 4;
     }
     if (!a.stream && a.tile_r == 0 && a.ldw != a.W) { g_sel_err = "psgla_tv_step: a row pitch ldw != W needs the streaming kernel"; return -1; }
     a.split_wgs = 0;

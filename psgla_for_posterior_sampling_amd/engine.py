@@ -37,7 +37,7 @@ class FusedTvChains:
         # rows padded to a multiple of 4 columns so that every width runs on the streaming kernel
         # (psgla_kernels.hip: ldw); the padding columns are scratch and every result is a view
         # of the first W columns
-        self.ldw = Wd if (Wd % 4 == 0 or kernel_variant in ("band", "tile")) else (Wd + 3) // 4 * 4
+        self.ldw = Wd if (Wd % 4 == 0 or kernel_variant in ("band", "tile", "wave")) else (Wd + 3) // 4 * 4
         self.pshape = (B, C, H, self.ldw)
         self.device = dev
         self.alpha = float(alpha)
@@ -88,7 +88,7 @@ class FusedTvChains:
         d.fresh = self.work.fresh.data_ptr()
         d.norms = self.work.norms.data_ptr()
         d.arrive = self.work.arrive.data_ptr()
-        d.kernel_variant = {"auto": 0, "band": 1, "stream": 2, "p2p": 3, "tile": 4}[kernel_variant]
+        d.kernel_variant = {"auto": 0, "band": 1, "stream": 2, "p2p": 3, "tile": 4, "wave": 5}[kernel_variant]
         d.stream_wgs = int(stream_wgs)
         self.desc = d
         self.sched_struct = self.sched.struct(True, 0)
@@ -172,7 +172,7 @@ class FusedTvChains:
         k = N.lib().psgla_tv_step_kernel(ctypes.byref(self.desc))
         if k < 0:
             raise RuntimeError(N.lib().psgla_last_error().decode())
-        return ("tv_main_kernel", "tv_stream_kernel", "tv_stream_kernel", "tv_tile_kernel")[k]
+        return ("tv_main_kernel", "tv_stream_kernel", "tv_stream_kernel", "tv_tile_kernel", "tv_wave_kernel")[k]
 
     def launch_main_only(self, n: int = 1):
         """Launch only the fused tile kernel n times for the CURRENT step (idempotent: it reads

@@ -730,3 +730,71 @@ def test_tile_kernel_equals_stream_kernel_full_size(B):
             outs.append((eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone()))
         for a, b in zip(*outs):
             assert torch.equal(a, b), f"exact={exact}"
+
+
+@pytest.mark.parametrize("B,H,W,alpha,tol,n_tv", [
+    (3, 48, 64, 1.0, 1e-5, 10),      # 3 ranges per plane: halo cuts at both ends
+    (2, 100, 64, 1.0, 1e-5, 10),     # 6 ranges per plane
+    (2, 77, 40, 0.6, 1e-5, 10),      # alpha != 1 (x2 state), narrow image (idle lanes)
+    (2, 40, 52, 1.0, 0.03, 10),      # deepinv's early stop (recompute by the last workgroup)
+    (2, 90, 256, 1.0, 1e-5, 3),      # n_tv < 10: general step body only
+    (1, 30, 20, 1.0, 1e-5, 7),       # whole planes (H < 32)
+])
+def test_wave_kernel_exact_vs_oracle(B, H, W, alpha, tol, n_tv):
+    """The per-wave pipeline kernel (each wave runs front, all inner iterations and back of its own row
+    range, state in registers) in exact mode: samples, block means and TV state bit-identical to the
+    CPU oracle for halo cuts inside planes, alpha != 1, early stop, n_tv < 10 and whole-plane ranges."""
+    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand((1, 3, H, W), generator=g)
+    dg, y, init, mask2d = orc.inpainting_problem(x, seed_ip=4)
+    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
+    n_iter = 14
+    eng = FusedTvChains(init.expand(B, -1, -1, -1).contiguous().to(DEV), y.to(DEV), mask2d.to(torch.uint8).to(DEV),
+                        c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)), alpha=alpha,
+                        ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=n_tv, tol=tol), seed=8,
+                        n_iter=n_iter, n_inter=3, n_inter_mmse=2, chain0=2, exact=True, kernel_variant="wave")
+    assert eng.main_kernel == "tv_wave_kernel"
+    eng.run(n_iter, graph_steps=6)
+    torch.cuda.synchronize()
+    bm, bm2 = eng.blocks()
+    for b in range(B):
+        tv = orc.TVDenoiser(n_it_max=n_tv, tol=tol)
+        Xl, Ml, M2l = orc.psgla(init, dg, tv, torch.tensor(alpha), torch.tensor(10.0), sig_float=10 / 255.0,
+                                delta=(10 / 255.0) ** 2, n_iter=n_iter, n_inter=3, n_inter_mmse=2, seed=8, chain=2 + b)
+        np.testing.assert_array_equal(eng.samples()[:, b].cpu().numpy(), np.stack([t.numpy() for t in Xl]))
+        np.testing.assert_array_equal(bm[:, b].cpu().numpy(), np.stack([t.numpy() for t in Ml]))
+        np.testing.assert_array_equal(bm2[:, b].cpu().numpy(), np.stack([t.numpy() for t in M2l]))
+        np.testing.assert_array_equal(eng.x2_state[b].cpu().numpy(), tv.x2.numpy()[0])
+        np.testing.assert_array_equal(eng.u2_state[b].cpu().numpy(), tv.u2.numpy()[0])
+
+
+@pytest.mark.parametrize("B,H,W", [(64, 256, 256), (4, 256, 256), (720, 32, 32)])
+def test_wave_kernel_equals_stream_kernel(B, H, W):
+    """The benched geometry (64 chains x 3 x 256 x 256: 2048 ranges of ~24 rows), a small batch (16
+    ranges per plane) and more planes than wave slots (whole planes, several per wave): the wave kernel
+    and the row-streaming kernel give bit-identical chains in both arithmetic modes."""
+    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    g = torch.Generator(device=DEV).manual_seed(4321)
+    xs = torch.rand((B, 3, H, W), generator=g, device=DEV)
+    gen = torch.Generator(device=DEV).manual_seed(0)
+    mask2d = (torch.rand((H, W), generator=gen, device=DEV) > 0.5).to(torch.uint8)
+    y = mask2d.float() * xs + torch.normal(torch.zeros_like(xs), std=(1 / 255.0) * torch.ones_like(xs),
+                                           generator=gen)
+    init = (mask2d.float() * y + (1 - mask2d.float()) * 0.5).contiguous()
+    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
+    for exact in (True, False):
+        outs = []
+        for variant in ("stream", "wave"):
+            eng = FusedTvChains(init, y.contiguous(), mask2d, c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
+                                alpha=1.0, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10), seed=0,
+                                n_iter=24, n_inter=10, n_inter_mmse=10, exact=exact, kernel_variant=variant)
+            eng.run(24, graph_steps=12)
+            torch.cuda.synchronize()
+            bm, bm2 = eng.blocks()
+            outs.append((eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone()))
+            del eng
+        for a, b in zip(*outs):
+            assert torch.equal(a, b), f"exact={exact}"
