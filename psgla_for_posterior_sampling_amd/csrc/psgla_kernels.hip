@@ -628,21 +628,31 @@ __device__ __forceinline__ void glds4(const void* src, void* dst) {
 // a 32-bit per-lane byte offset in one VGPR -- no 64-bit per-lane address stays live across the row loop
 // (a spilled one is reloaded behind a compiler vmcnt(0) that serialises the hand-placed DMAs).  No
 // immediate offsets (an LDS-DMA's would also move its LDS destination).
+// The base is wave-uniform by construction at every call site; readfirstlane makes that provable where
+// the compiler cannot see it (free when the value already sits in SGPRs).  The asm opens with s_nop 4:
+// a VMEM instruction reading an SGPR that a VALU (v_readfirstlane) wrote needs 5 wait states, and the
+// compiler does not pad hazards into inline asm (without it the loads read a stale base: memory fault).
+__device__ __forceinline__ const void* uni_ptr(const void* p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (const void*)(((uint64_t)hi << 32) | lo);
+}
 // 16 B (4 B) per lane straight into LDS: lane i lands at dst + 16 i (4 i)
 __device__ __forceinline__ void sglds16(const void* sbase, uint32_t voff, void* dst) {
     const unsigned m = (unsigned)(size_t)(lptr_t)dst;
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
-                 :: "v"(voff), "s"(sbase), "s"(m) : "memory", "m0");
+    asm volatile("s_nop 4\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                 :: "v"(voff), "s"(uni_ptr(sbase)), "s"(m) : "memory", "m0");
 }
 __device__ __forceinline__ void sglds4(const void* sbase, uint32_t voff, void* dst) {
     const unsigned m = (unsigned)(size_t)(lptr_t)dst;
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1"
-                 :: "v"(voff), "s"(sbase), "s"(m) : "memory", "m0");
+    asm volatile("s_nop 4\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1"
+                 :: "v"(voff), "s"(uni_ptr(sbase)), "s"(m) : "memory", "m0");
 }
 // 16-B streaming (nt) store; s_nop: the store-data hazard the compiler cannot see
 __device__ __forceinline__ void sgst16(void* sbase, uint32_t voff, const float4& v) {
     const v4f_t x = {v.x, v.y, v.z, v.w};
-    asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 1" :: "v"(voff), "v"(x), "s"(sbase) : "memory");
+    asm volatile("s_nop 4\n\tglobal_store_dwordx4 %0, %1, %2 nt\n\ts_nop 1" :: "v"(voff), "v"(x), "s"(uni_ptr(sbase)) : "memory");
 }
 // Workgroup barrier that only drains LDS (lgkmcnt): LDS-DMA loads stay in flight across it
 // (a __syncthreads() fence would wait vmcnt(0) while a global_load_lds is pending).
@@ -1283,6 +1293,9 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
             const SegGeo g = seg_geo<GEN>(a, rc.p);
             const int gjr = GEN ? min(g.f0 + CPL * lane, L - CPL) : gjc;
             const int bb = g.rp / C;
+#ifndef PSGLA_STREAM_SADDR
+            // 64-bit per-lane addresses (default; the SGPR-base form, -DPSGLA_STREAM_SADDR, measured +12 %:
+            // this kernel's row cursor sits in VGPRs, so each DMA pays two readfirstlane + 5 wait states)
             const size_t base = plane_off(g.rp) + (size_t)rr * L + gjr;
             if (part == 0) {
                 glds16(xin + base, &sh.fst[fw][bi][0][0]);
@@ -1296,6 +1309,23 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                 if (!ALPHA1) glds16(x2in + base, &sh.fst[fw][bi][4][0]);
                 glds4(a.mask + (size_t)bb * a.m_cs + (size_t)rr * L + gjr, &sh.fmk[fw][bi][0]);
             }
+#else
+            // the row's base in SGPRs (saddr), the lane's column as a 32-bit byte offset
+            const size_t rb = plane_off(g.rp) + (size_t)rr * L;
+            const uint32_t vo = (uint32_t)gjr * 4u;
+            if (part == 0) {
+                sglds16(xin + rb, vo, &sh.fst[fw][bi][0][0]);
+            } else if (part == 1) {
+                sglds16(a.yobs + (size_t)bb * a.y_cs + (size_t)(g.rp - bb * C) * HW + (size_t)rr * L, vo,
+                        &sh.fst[fw][bi][1][0]);
+            } else if (part == 2) {
+                sglds16(u2in + 2 * rb, 2u * vo, &sh.fst[fw][bi][2][0]);
+                sglds16(u2in + 2 * rb + 4, 2u * vo, &sh.fst[fw][bi][3][0]);
+            } else {
+                if (!ALPHA1) sglds16(x2in + rb, vo, &sh.fst[fw][bi][4][0]);
+                sglds4(a.mask + (size_t)bb * a.m_cs + (size_t)rr * L, (uint32_t)gjr, &sh.fmk[fw][bi][0]);
+            }
+#endif
         };
         // row fw's loads up front; afterwards the loads of row q + 4 are issued one part per
         // phase of row q (into the buffer of row q - 4, consumed before phase 0 of row q), so
@@ -1454,19 +1484,27 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                 const int bi = (q >> 1) & 1;
                 const SegGeo g = seg_geo<GEN>(a, rc.p);
                 const int gjr = GEN ? min(g.f0 + CPL * lane, L - CPL) : gjc;
+#ifndef PSGLA_STREAM_SADDR
                 const size_t base = plane_off(g.rp) + (size_t)rr * L + gjr;
                 glds16(mean_in + base, &sh.bst[bw][bi][0][0]);
                 glds16(sq_in + base, &sh.bst[bw][bi][1][0]);
+#else
+                const size_t rb = plane_off(g.rp) + (size_t)rr * L;
+                sglds16(mean_in + rb, (uint32_t)gjr * 4u, &sh.bst[bw][bi][0][0]);
+                sglds16(sq_in + rb, (uint32_t)gjr * 4u, &sh.bst[bw][bi][1][0]);
+#endif
             }
         };
         // vector-memory stores per core row (all lanes of a wave store together; lane 0 is core)
         const int nst = 3 + (ALPHA1 ? 0 : 1) + ((si.acc && (si.blockend || si.liveout)) ? 2 : 0) + (si.sample ? 1 : 0);
         // a row's stores are spread over the wave's two steps: state + accumulators, then the rest
         bool hold = false, hcore = core;
-        size_t h_base = 0;
+        size_t h_base = 0;                  // per-lane element index (PSGLA_STREAM_SADDR: the row's uniform base)
+        uint32_t h_vo = 0;                  // the lane's column as a byte offset
         float4 hM = zero4, hQ = zero4, hX = zero4;
         auto flush_held = [&]() {
             if (!(GEN ? hcore : core)) return;
+#ifndef PSGLA_STREAM_SADDR
             if (si.acc) {
                 if (si.blockend) {
                     st_nt(a.blocks + (size_t)si.blk * BE + h_base, hM);
@@ -1477,6 +1515,18 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                 }
             }
             if (si.sample) st_nt(a.samples + (size_t)si.sidx * BE + h_base, hX);
+#else
+            if (si.acc) {
+                if (si.blockend) {
+                    sgst16(a.blocks + (size_t)si.blk * BE + h_base, h_vo, hM);
+                    sgst16(a.blocks2 + (size_t)si.blk * BE + h_base, h_vo, hQ);
+                } else if (si.liveout) {
+                    sgst16(a.mean[par_out] + h_base, h_vo, hM);
+                    sgst16(a.sq[par_out] + h_base, h_vo, hQ);
+                }
+            }
+            if (si.sample) sgst16(a.samples + (size_t)si.sidx * BE + h_base, h_vo, hX);
+#endif
         };
         // mean / sq rows are LDS-DMA'd two of the wave's rows ahead (4 stream rows); c1 / c2 =
         // vector-memory ops issued after the DMA of the wave's next / next-but-one row
@@ -1555,6 +1605,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                     const SegGeo gr = seg_geo<GEN>(a, rc.p);
                     const int gjr = GEN ? gr.f0 + CPL * lane : gj0;
                     const bool corer = GEN ? (gjr < W && gjr >= gr.cc0 && gjr < gr.cc1) : core;
+#ifndef PSGLA_STREAM_SADDR
                     if (rowcore && corer) {
                         const size_t base = plane_off(gr.rp) + (size_t)rc.r * L + gjr;
                         st_nt(a.x[par_out] + base, Xo);
@@ -1565,6 +1616,19 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                         // the accumulator / sample stores go out in the wave's next (idle) step
                         h_base = base; hM = M4; hQ = Q4; hX = Xo;
                     }
+#else
+                    const size_t rb = plane_off(gr.rp) + (size_t)rc.r * L;   // the row's base (uniform)
+                    const uint32_t vo = (uint32_t)gjr * 4u;
+                    if (rowcore) { h_base = rb; h_vo = vo; }
+                    if (rowcore && corer) {
+                        sgst16(a.x[par_out] + rb, vo, Xo);
+                        sgst16(a.u2[par_out] + 2 * rb, 2u * vo, make_float4(U0.x, U1.x, U0.y, U1.y));
+                        sgst16(a.u2[par_out] + 2 * rb + 4, 2u * vo, make_float4(U0.z, U1.z, U0.w, U1.w));
+                        if (!ALPHA1) sgst16(a.x2[par_out] + rb, vo, X2);
+                        // the accumulator / sample stores go out in the wave's next (idle) step
+                        hM = M4; hQ = Q4; hX = Xo;
+                    }
+#endif
                     hold = rowcore;
                     if (GEN) hcore = corer;
                 } else if (hold) {
