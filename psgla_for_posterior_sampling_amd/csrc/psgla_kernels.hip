@@ -123,6 +123,11 @@ __device__ __forceinline__ float wave_sum(float v) {
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
     return v;
 }
+__device__ __forceinline__ float2 row_sum2(float a, float b) {
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) { a += __shfl_xor(a, o); b += __shfl_xor(b, o); }
+    return make_float2(a, b);
+}
 #else
 #define PSGLA_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), (ctrl), 0xF, 0xF, false))
 __device__ __forceinline__ float wave_sum(float v) {
@@ -135,6 +140,14 @@ __device__ __forceinline__ float wave_sum(float v) {
     const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
     const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
     return (r0 + r1) + (r2 + r3);
+}
+// Sums over each 16-lane row, returned in every lane of the row (the first 4 steps of wave_sum).
+__device__ __forceinline__ float2 row_sum2(float a, float b) {
+    a += PSGLA_DPP(a, 0xB1); b += PSGLA_DPP(b, 0xB1);      // quad_perm [1,0,3,2]
+    a += PSGLA_DPP(a, 0x4E); b += PSGLA_DPP(b, 0x4E);      // quad_perm [2,3,0,1]
+    a += PSGLA_DPP(a, 0x124); b += PSGLA_DPP(b, 0x124);    // row_ror:4
+    a += PSGLA_DPP(a, 0x128); b += PSGLA_DPP(b, 0x128);    // row_ror:8
+    return make_float2(a, b);
 }
 #undef PSGLA_DPP
 #endif
@@ -691,6 +704,9 @@ __device__ __forceinline__ void st_nt(float* p, const float4& v) {
 // and each then releases (writes back) its XCD's dirty L2 lines before the arrival count, which
 // write-through stores leave clean; -DPSGLA_TILE_ST_NT: nt stores as the stream kernel.
 __device__ __forceinline__ void st_tile(float* p, const float4& v) {
+#ifdef PSGLA_ABL_NOSTORE
+    if (p) return;      // diagnostic timing build only: outputs are not written
+#endif
 #if defined(PSGLA_TILE_ST_NT)
     st_nt(p, v);
 #else
@@ -1778,7 +1794,7 @@ struct TileShared {
     float4 zrow[TV_NW][WAVE];          // first-row z of each wave (read by the wave above)
     float4 urow[TV_NW][WAVE];          // last-row u2[..., 0] of each wave (read by the wave below)
     float4 mst[TV_NW * R][2][WAVE];    // mean / sq rows of the tile (LDS-DMA at the start)
-    float red[MAXIT][TV_NW][2];        // per-wave rel_err partial sums
+    float2 red[MAXIT][TV_NW][4];       // rel_err partial sums per (iteration, wave, 16-lane row of the wave)
     int s_stop[MAXG];
     int s_flag, s_item, s_next;
 };
@@ -1883,8 +1899,15 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
     // for the dual and one row more below for the primal (the dual of a row reads the next row's z);
     // a wave none of whose rows is needed skips the phase (its stale rows feed only unneeded rows).
     const int wr0 = e0 + w * R, wr1 = wr0 + R;
+#ifdef PSGLA_ABL_TILE_NOITER
+    n_it = 0;            // diagnostic timing build only: loads, noise, data term and stores
+#endif
     for (int it = 0; it < n_it; ++it) {
+#ifdef PSGLA_ABL_TILE_NOTRK
+        const bool trk = false;   // diagnostic timing build only
+#else
         const bool trk = track && it >= trk_lo(a) && it <= trk_hi(a);
+#endif
         float sd = 0.f, sn = 0.f;
         const int span = n_it - 1 - it;
         const bool act_p = wr1 > r0 - span && wr0 < r1 + span + 1;
@@ -1913,18 +1936,18 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
                     zv = __builtin_fmaf(2.0f, xv, -xo);
                     xn = __builtin_fmaf(a.rho, xv - xo, xo);
                 }
-                if (trk) {
-                    const bool cnt = core[r] && rv[r] && colok;
+                // rel-err terms of the counted rows (row-uniform test; lanes past W are masked once, at
+                // the reduction: adding nothing and adding +0 leave a lane's sum identical)
+                if (trk && core[r] && rv[r]) {
                     if (EXACT) {
-                        const float d = cnt ? xo - xn : 0.f;
-                        const float q = cnt ? xn + 1e-12f : 0.f;
+                        const float d = xo - xn;
+                        const float q = xn + 1e-12f;
                         sd = __builtin_fmaf(d, d, sd);
                         sn = __builtin_fmaf(q, q, sn);
                     } else {
-                        const float d = cnt ? xv - xo : 0.f;
-                        const float q = cnt ? xn : 0.f;
+                        const float d = xv - xo;
                         sd = __builtin_fmaf(d, d, sd);
-                        sn = __builtin_fmaf(q, q, sn);
+                        sn = __builtin_fmaf(xn, xn, sn);
                     }
                 }
                 z[r][k] = zv;
@@ -1933,12 +1956,14 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
         }
         if (act_p) sh.zrow[w][lane] = make_float4(z[0][0], z[0][1], z[0][2], z[0][3]);
         if (trk) {
-            sd = wave_sum(sd);
-            sn = wave_sum(sn);
-            if (!EXACT) sd *= a.rho * a.rho;          // fast sums hold (x - x2_prev)^2
-            if (lane == 0) { sh.red[it][w][0] = sd; sh.red[it][w][1] = sn; }
+            // 16-lane row sums by 4 DPP steps (no readlane round trip before the barrier); the 4 row sums of
+            // each wave meet the other waves' at the end of the tile
+            const float2 rs = row_sum2(colok ? sd : 0.f, colok ? sn : 0.f);
+            if ((lane & 15) == 0) sh.red[it][w][lane >> 4] = rs;
         }
+#ifndef PSGLA_ABL_TILE_NOBAR
         __syncthreads();
+#endif
         // dual: u = prox_sigma_g_conj(u2 + sigma nabla z, ths); u2 += rho (u - u2)
         const float4 dn = (w < TV_NW - 1) ? sh.zrow[w + 1][lane] : zero4;
 #pragma unroll
@@ -1974,14 +1999,18 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
             }
         }
         if (act_d) sh.urow[w][lane] = make_float4(u0[R - 1][0], u0[R - 1][1], u0[R - 1][2], u0[R - 1][3]);
+#ifndef PSGLA_ABL_TILE_NOBAR
         __syncthreads();
+#endif
     }
     // ---- 5. rel_err partial sums -> the chain's norms (one fp64 atomic per iteration and workgroup)
     if (track) {
         const int t = threadIdx.x;
         if (t >= trk_lo(a) && t <= trk_hi(a) && t < n_it) {
             double sd = 0.0, sn = 0.0;
-            for (int ww = 0; ww < TV_NW; ++ww) { sd += sh.red[t][ww][0]; sn += sh.red[t][ww][1]; }
+            for (int ww = 0; ww < TV_NW; ++ww)
+                for (int q = 0; q < 4; ++q) { sd += sh.red[t][ww][q].x; sn += sh.red[t][ww][q].y; }
+            if (!EXACT) sd *= (double)(a.rho * a.rho);     // fast sums hold (x - x2_prev)^2
             atomicAdd(&a.norms[((size_t)b * a.n_tv + t) * 2], sd);
             atomicAdd(&a.norms[((size_t)b * a.n_tv + t) * 2 + 1], sn);
         }
