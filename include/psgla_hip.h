@@ -81,7 +81,11 @@ typedef struct PsglaSchedule {
  *     finalised by its last workgroup like the stream kernel;
  *   - otherwise (n_tv > 10 or H < 2, or kernel_variant 1) the temporally blocked
  *     band kernel (tv_main_kernel) followed by a small finaliser kernel
- *     (tv_finalise_kernel, <= 8 workgroups) that does the same.
+ *     (tv_finalise_kernel, <= 8 workgroups) that does the same;
+ *   - only when forced (kernel_variant 5; W <= 256, W % 4 == 0, ldw == W, 1 <= n_tv <= 10,
+ *     H >= 2) the per-wave pipeline kernel (tv_wave_kernel: each wave runs front, all inner
+ *     iterations and back of its own row range of one plane, state in registers; ONE launch,
+ *     finalised by its last workgroup; slower than the stream kernel at 64 chains).
  * launch_mask 1 launches only the main pass of either variant (timing).
  * ------------------------------------------------------------------------------- */
 typedef struct PsglaTvStep {
@@ -114,7 +118,8 @@ typedef struct PsglaTvStep {
                                  else temporally blocked bands); 1: force bands; 2: force stream
                                  (one workgroup barrier per pipeline step); 3: force stream with
                                  point-to-point LDS progress waits instead of the barrier; 4: force
-                                 the small-batch tile kernel (W <= 256, W % 4 == 0, ldw == W).  Auto
+                                 the small-batch tile kernel (W <= 256, W % 4 == 0, ldw == W); 5: force
+                                 the per-wave pipeline kernel (same shape limits, 1 <= n_tv <= 10).  Auto
                                  picks the tile kernel when its tiles (one per workgroup, 48 rows
                                  incl. n_tv halo rows) all fit on the CUs at once, else the stream */
     uint64_t* debug_stamps;   /* diagnostic builds only (-DPSGLA_STAMPS), else NULL: [workgroups][16][2]
@@ -135,7 +140,8 @@ typedef struct PsglaTvStep {
 int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream);
 /* Which kernel psgla_tv_step launches for this descriptor (host-side query, launches nothing):
  * 0 band kernel + finaliser, 1 row stream, 2 row stream with P2P waits, 3 small-batch tile kernel
- * (one launch, finalised by its last workgroup); -1 if the descriptor is rejected. */
+ * (one launch, finalised by its last workgroup), 4 per-wave pipeline kernel (one launch, finalised by
+ * its last workgroup); -1 if the descriptor is rejected. */
 int psgla_tv_step_kernel(const PsglaTvStep* d);
 
 /* ---------------------------------------------------------------------------------
