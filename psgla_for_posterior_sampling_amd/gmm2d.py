@@ -93,29 +93,39 @@ def _data_score(y, x, A, sigma):
     return A.T @ (y - A @ x) / sigma ** 2
 
 
-def pnp_ula(N, x_0, y, delta, A, sigma, denoiser, epsilon, alpha):
+def pnp_ula(N, x_0, y, delta, A, sigma, denoiser, epsilon, alpha, post=None, metric_each_step=False):
     """PnP-ULA, N - 1 steps from x_0 (sampling_2D.py:22-46):
-    x' = x + delta s(y|x) + alpha delta (D(x, eps) - x)/eps + sqrt(2 delta) z."""
+    x' = x + delta s(y|x) + alpha delta (D(x, eps) - x)/eps + sqrt(2 delta) z.
+    metric_each_step (sampling_2D.py:38-39): after step i with i % 100 == 0, the Wasserstein distance
+    between the chain so far and as many posterior samples (`post`); its sub-sampling draws come from
+    the same global numpy stream, so the chain differs from a run without metrics, as in the reference.
+    Returns X, or (X, distances) with metric_each_step."""
     X = [x_0]
     x = x_0
-    for _ in range(N - 1):
+    W = []
+    for i in range(N - 1):
         z = np.random.randn(y.shape[0])
         x = x + delta * _data_score(y, x, A, sigma) + alpha * delta * (1 / epsilon) * (denoiser(x, epsilon) - x) \
             + np.sqrt(2 * delta) * z
         X.append(x)
-    return np.array(X)
+        if metric_each_step and i % 100 == 0:
+            W.append(wasserstein2(np.array(X), post[:len(X), :]))
+    return (np.array(X), W) if metric_each_step else np.array(X)
 
 
-def snopnp_ula(N, x_0, y, delta, A, sigma, denoiser, alpha):
+def snopnp_ula(N, x_0, y, delta, A, sigma, denoiser, alpha, post=None, metric_each_step=False):
     """SnoPnP-ULA -- the 2-D PSGLA: x' = D(x + (delta/alpha) s(y|x) + sqrt(2 delta) z, delta)
-    (sampling_2D.py:49-70)."""
+    (sampling_2D.py:49-70); metric_each_step as pnp_ula (sampling_2D.py:65-66)."""
     X = [x_0]
     x = x_0
-    for _ in range(N - 1):
+    W = []
+    for i in range(N - 1):
         z = np.random.randn(y.shape[0])
         x = denoiser(x + (delta / alpha) * _data_score(y, x, A, sigma) + np.sqrt(2 * delta) * z, delta)
         X.append(x)
-    return np.array(X)
+        if metric_each_step and i % 100 == 0:
+            W.append(wasserstein2(np.array(X), post[:len(X), :]))
+    return (np.array(X), W) if metric_each_step else np.array(X)
 
 
 def wasserstein2(sample1, sample2, n: int = 1000):
@@ -164,9 +174,11 @@ def density_mse(sample, mus, covs, w):
     return float(np.sum((Z - P) ** 2))
 
 
-def run_experiment(name: str = "symetric_gaussians", N: int = 1000, seed: int = 0, metrics: bool = True):
+def run_experiment(name: str = "symetric_gaussians", N: int = 1000, seed: int = 0, metrics: bool = True,
+                   metric_each_step: bool = False):
     """The body of sampling_2D.py:72-250 for one N (plots omitted): returns the result dict the
-    reference np.saves (same keys)."""
+    reference np.saves (same keys; with metric_each_step also 'Wass_dist_ULA_list' and
+    'Wass_dist_PSGLA_list', sampling_2D.py:246-248)."""
     np.random.seed(seed)
     mu_list, sigma_list, pi_list = gaussian_mixt_example(name)
     A = np.eye(2)
@@ -179,10 +191,26 @@ def run_experiment(name: str = "symetric_gaussians", N: int = 1000, seed: int = 
     for y in Y:
         post.append(sample_posterior(A, y, sigma, N, mu_list, sigma_list, pi_list))
         post2.append(sample_posterior(A, y, sigma, N, mu_list, sigma_list, pi_list))
-    ula = [pnp_ula(N, Y[i], Y[i], delta_pnp, A, sigma, D, eps_pnp, alpha_pnp) for i in range(3)]
-    for i in range(3):                      # the plot's sub-sampling draws (sampling_2D.py:104)
+    wula, wsno = [], []
+    if metric_each_step:
+        ula = []
+        for i in range(3):
+            xs, ws = pnp_ula(N, Y[i], Y[i], delta_pnp, A, sigma, D, eps_pnp, alpha_pnp, post=post[i],
+                             metric_each_step=True)
+            ula.append(xs)
+            wula.append(ws)
+    else:
+        ula = [pnp_ula(N, Y[i], Y[i], delta_pnp, A, sigma, D, eps_pnp, alpha_pnp) for i in range(3)]
+    for i in range(3):                      # the plot's sub-sampling draws (sampling_2D.py:114)
         np.random.permutation(ula[i])
-    sno = [snopnp_ula(N, Y[i], Y[i], delta_sno, A, sigma, D, alpha_sno) for i in range(3)]
+    if metric_each_step:
+        sno = []
+        for i in range(3):
+            xs, ws = snopnp_ula(N, Y[i], Y[i], delta_sno, A, sigma, D, alpha_sno, post=post[i], metric_each_step=True)
+            sno.append(xs)
+            wsno.append(ws)
+    else:
+        sno = [snopnp_ula(N, Y[i], Y[i], delta_sno, A, sigma, D, alpha_sno) for i in range(3)]
     for i in range(3):
         np.random.permutation(sno[i])
     out = {"A": A, "mu_list": mu_list, "sigma_list": sigma_list, "pi_list": pi_list, "sigma": sigma,
@@ -204,6 +232,9 @@ def run_experiment(name: str = "symetric_gaussians", N: int = 1000, seed: int = 
             mus, cov, w = posterior_constants(A, Y[i], sigma, mu_list, sigma_list, pi_list)
             out["MMSE_PnP_ULA"].append(density_mse(ula[i], mus, cov, w))
             out["MMSE_SnoPnP_ULA"].append(density_mse(sno[i], mus, cov, w))
+    if metric_each_step:
+        out["Wass_dist_ULA_list"] = wula
+        out["Wass_dist_PSGLA_list"] = wsno
     return out
 
 
@@ -218,12 +249,10 @@ def main(argv=None):
     p.add_argument("--metric_each_step", type=bool, default=False)
     p.add_argument("--results_root", type=str, default="results")
     pars = p.parse_args(argv)
-    if pars.metric_each_step:
-        raise NotImplementedError("--metric_each_step: per-step Wasserstein curves are not part of this build")
     path = os.path.join(pars.results_root, "result_GMM")
     os.makedirs(path, exist_ok=True)
     for N in ([100, 1000, 10000] if pars.N is None else [pars.N]):
-        res = run_experiment(pars.name, N)
+        res = run_experiment(pars.name, N, metric_each_step=pars.metric_each_step)
         for i in range(3):
             print("Observation " + str(i))
             print("Sliced Wasserstein for PnP ULA = {:.2f} and SnoPnP ULA = {:.2f} and reference dist = {:.2f}".format(

@@ -49,3 +49,19 @@ def test_cli_writes_result(tmp_path):
     assert f.exists()
     d = np.load(f, allow_pickle=True).item()       # written by this test
     assert set(res) == set(d) and len(d["Sample_SnoPnP_ULA"]) == 3 and d["Sample_PnP_ULA"][0].shape == (100, 2)
+
+
+def test_metric_each_step_matches_reference():
+    """--metric_each_step (sampling_2D.py:38-39, 65-66): the per-100-step Wasserstein calls draw from
+    the global numpy stream, so the chains differ from a plain run; the samples of that run match the
+    reference's own samplers bit for bit (tests/golden/make_golden_2d.py --metric_each_step).  The
+    distance values use the same exact EMD on both sides (POT is absent: parity unpinned against it)."""
+    fx = dict(np.load(os.path.join(G, "gmm2d_each_step_N250.npz"), allow_pickle=False))
+    res = gmm2d.run_experiment("symetric_gaussians", 250, seed=0, metrics=False, metric_each_step=True)
+    for i in range(3):
+        np.testing.assert_array_equal(res["Sample_PnP_ULA"][i], fx[f"ula{i}"])
+        np.testing.assert_array_equal(res["Sample_SnoPnP_ULA"][i], fx[f"sno{i}"])
+        assert len(res["Wass_dist_ULA_list"][i]) == 3 and len(res["Wass_dist_PSGLA_list"][i]) == 3
+        np.testing.assert_allclose(res["Wass_dist_ULA_list"][i], fx[f"wula{i}"], rtol=1e-12)
+        np.testing.assert_allclose(res["Wass_dist_PSGLA_list"][i], fx[f"wsno{i}"], rtol=1e-12)
+    np.testing.assert_array_equal(np.random.rand(4), fx["next_uniform"])
