@@ -251,6 +251,29 @@ def blur_operators(l: int = 4, blur_type: str = "uniform", si: float = 1.0, chan
     return A, AT
 
 
+def blur_grad_tap_order(x: np.ndarray, y: np.ndarray, hconv: np.ndarray, hcorr: np.ndarray, l: int,
+                        sigma2: float) -> np.ndarray:
+    """-AT(A x - y) / sigma2 of ``blur_operators`` (sampling_images.py:329-338) with every output's
+    (2l+1)^2-term sums taken in (row, column) tap order, one fp32 rounding per product and per sum --
+    the order the HIP stencil's exact mode uses.  torch's CPU conv2d order is unspecified, so the
+    reference closure itself is only matched to a tolerance; this restatement pins the kernel bit for bit.
+    x, y: float32 (..., H, W); taps float32 (2l+1, 2l+1)."""
+    K = 2 * l + 1
+    hconv = np.asarray(hconv, np.float32)
+    hcorr = np.asarray(hcorr, np.float32)
+
+    def corr(v, h):
+        acc = np.zeros_like(v)
+        for u in range(K):
+            for w in range(K):
+                # conv2d(pad(v, l, circular), h)[i, j] = sum_{u,w} h[u, w] v[(i + u - l) % H, (j + w - l) % W]
+                acc = acc + h[u, w] * np.roll(v, shift=(l - u, l - w), axis=(-2, -1))
+        return acc
+
+    r = corr(np.asarray(x, np.float32), hconv) - np.asarray(y, np.float32)
+    return (-corr(r, hcorr)) / np.float32(sigma2)
+
+
 def deblurring_problem(im_t: torch.Tensor, seed_ip: int = 0, l: int = 4, blur_type: str = "uniform",
                        si: float = 1.0, sigma: float = 1.0):
     """Circular (2l+1)^2 deblurring: returns (data_grad, y_t, init)."""
@@ -380,6 +403,6 @@ def psgla_coefficients(delta_float: float, lambd: float, s: float):
 
 __all__ = [
     "normal", "philox4x32_10", "radius_table", "angle_table", "TVDenoiser", "ClampDenoiser",
-    "TinyConvDenoiser", "inpainting_problem", "blur_kernel", "blur_operators", "deblurring_problem",
+    "TinyConvDenoiser", "inpainting_problem", "blur_kernel", "blur_operators", "blur_grad_tap_order", "deblurring_problem",
     "psgla", "pnpula", "mmse_of_blocks", "psgla_params_tv", "psgla_coefficients", "math",
 ]

@@ -2712,15 +2712,29 @@ __global__ void langevin_update_kernel(const float* X, const float* g, float* Y,
 // ---------------------------------------------------------------------------------------
 // Deblurring data term (sampling_images.py:304-341): g = -A^T(A x - y) / sigma2 with
 // A x = conv2d(pad(x, l, circular), hconv) and A^T r = conv2d(pad(r, l, circular), hcorr),
-// depthwise, K = 2l+1 taps per side (the same for every channel).  One workgroup per 32 x 64
-// output tile of a plane: x is staged in LDS with a 2l halo (circular wrap on load), r = A x - y
-// is formed in LDS on the tile + l halo, then g = -(A^T r) / sigma2.  Register blocking: a
-// thread produces 4 adjacent columns from one (4 + 2l)-wide LDS row segment per tap row
-// (ds_read_b128), and the taps are kernel arguments (compile-time indices -> SGPR operands).
-// With Y != NULL the Langevin update Y = (X + c1 g) + c2 Z is fused (g is never stored).
+// depthwise, K = 2l+1 taps per side (the same for every channel).  One workgroup per 64 x 64
+// output tile of a plane: x is staged in LDS with a 2l halo (circular wrap on load, 16-byte loads
+// where the tile does not wrap), r = A x - y is formed in LDS on the tile + l halo, then
+// g = -(A^T r) / sigma2.  Register blocking over rows AND columns: a thread produces a 4-column x
+// M-row block, reading each of its M + 2l input rows once (ceil((4 + 2l) / 4) ds_read_b128) and
+// adding that row into every output row it touches -- LDS traffic per output falls from
+// K x (4 + 2l) floats / 4 to (M + 2l) x (4 + 2l) / (4 M), so the 2 x K^2 multiply-adds (VALU), not
+// LDS, bound the kernel.  Every output's sum still runs over (u, v) in increasing order (the same
+// arithmetic as a plain per-output loop; `oracle.blur_grad_tap_order` pins it bit for bit in exact
+// mode).  The taps are kernel arguments (compile-time indices -> SGPR operands).
+// With Y != NULL the Langevin update Y = (X + c1 g) + c2 Z is fused (g is never stored; X is read
+// from the staged tile).
 // ---------------------------------------------------------------------------------------
-constexpr int BL_TH = 32, BL_TW = 64, BL_MAXL = 8, BL_THREADS = 256;
+constexpr int BL_TH = 64, BL_TW = 64, BL_MAXL = 8, BL_THREADS = 256;
 constexpr int BL_MAXK = 2 * BL_MAXL + 1;
+constexpr int BL_MG = 4;                          // output rows per thread in the A^T r pass (16 x 16 blocks)
+
+// rows per thread of the r = A x - y pass: the smallest M >= 4 whose blocks fit one pass of the workgroup
+__host__ __device__ constexpr int bl_mr(int L) {
+    int m = 4;
+    while (m < 16 && ((BL_TW + 2 * L + 3) / 4) * ((BL_TH + 2 * L + m - 1) / m) > BL_THREADS) ++m;
+    return m;
+}
 
 struct BlurArgs {
     const float* X;
@@ -2736,117 +2750,231 @@ struct BlurArgs {
     int chain0;
     const long long* d_step;
     long long off;
-    int tiles_x;
+    int tiles_x, tiles_y;
 };
 
-template <bool EXACT, int L>
-__global__ void __launch_bounds__(BL_THREADS) blur_grad_kernel(const BlurArgs a) {
-    constexpr int K = 2 * L + 1;
-    constexpr int XH = BL_TH + 4 * L, XW = BL_TW + 4 * L;
-    constexpr int RH = BL_TH + 2 * L, RW = BL_TW + 2 * L;
-    constexpr int XS = ((XW + 3) & ~3) + 4, RS = ((RW + 3) & ~3) + 4;   // 16-B aligned row strides
-    constexpr int SEG = (4 + 2 * L + 3) / 4;                            // float4 reads per row segment
-    __shared__ __attribute__((aligned(16))) float xs[XH * XS];
-    __shared__ __attribute__((aligned(16))) float rs[RH * RS];
-    const int H = a.H, W = a.W;
-    const int plane = blockIdx.y, b = plane / a.C, c = plane - b * a.C;
-    const int ty = blockIdx.x / a.tiles_x, tx = blockIdx.x - ty * a.tiles_x;
-    const int i0 = ty * BL_TH, j0 = tx * BL_TW;
-    const size_t HW = (size_t)H * W;
-    const float* xp = a.X + (size_t)plane * HW;
-    const float* yp = a.y + (size_t)b * a.y_cs + (size_t)c * HW;
-    // circular index; offsets are within 2l <= 16 of the plane, so this rarely loops (no division)
-    auto wrap = [](int v, int n) { while (v < 0) v += n; while (v >= n) v -= n; return v; };
-    // x on rows i0-2l .. i0+TH+2l-1, cols j0-2l .. j0+TW+2l-1 (circular padding applied twice)
-    for (int t = threadIdx.x; t < XH * XW; t += BL_THREADS) {
-        const int p = t / XW, q = t - p * XW;
-        xs[p * XS + q] = xp[(size_t)wrap(i0 - 2 * L + p, H) * W + wrap(j0 - 2 * L + q, W)];
-    }
-    __syncthreads();
-    // r = A x - y on rows i0-l .. i0+TH+l-1, cols j0-l .. j0+TW+l-1: strips of 4 columns
-    constexpr int RQ = (RW + 3) / 4;
-    for (int t = threadIdx.x; t < RH * RQ; t += BL_THREADS) {
-        const int p = t / RQ, q = (t - p * RQ) * 4;
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+// acc[m][0..3] += sum_v h[u][v] * row[k + v] for every output row m that input row `ir` feeds (u = ir - m)
+template <bool EXACT, int K, int M, int SEG>
+__device__ __forceinline__ void bl_row_accumulate(const float* __restrict__ h, const float (&row)[SEG * 4], int ir,
+                                                  float (&acc)[M][4]) {
 #pragma unroll
-        for (int u = 0; u < K; ++u) {
-            float row[SEG * 4];
+    for (int m = 0; m < M; ++m) {
+        const int u = ir - m;
+        if (u < 0 || u >= K) continue;                 // compile-time after unrolling
 #pragma unroll
-            for (int sg = 0; sg < SEG; ++sg) {
-                const float4 v = *reinterpret_cast<const float4*>(&xs[(p + u) * XS + q + 4 * sg]);
-                row[4 * sg] = v.x; row[4 * sg + 1] = v.y; row[4 * sg + 2] = v.z; row[4 * sg + 3] = v.w;
-            }
-#pragma unroll
-            for (int v = 0; v < K; ++v) {
-                const float hv = a.hconv[u * K + v];
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    acc[k] = EXACT ? acc[k] + hv * row[k + v] : __builtin_fmaf(hv, row[k + v], acc[k]);
-            }
-        }
-        const int gi = wrap(i0 - L + p, H);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (q + k < RW) rs[p * RS + q + k] = acc[k] - yp[(size_t)gi * W + wrap(j0 - L + q + k, W)];
-    }
-    __syncthreads();
-    // g = -(A^T r) / sigma2 on the tile (+ the fused Langevin update)
-    const long long step = (a.d_step ? *a.d_step : 0LL) + a.off;
-    constexpr int TQ = BL_TW / 4;
-    for (int t = threadIdx.x; t < BL_TH * TQ; t += BL_THREADS) {
-        const int p = t / TQ, q = (t - p * TQ) * 4;
-        const int i = i0 + p, j = j0 + q;
-        if (i >= H || j >= W) continue;
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int u = 0; u < K; ++u) {
-            float row[SEG * 4];
-#pragma unroll
-            for (int sg = 0; sg < SEG; ++sg) {
-                const float4 v = *reinterpret_cast<const float4*>(&rs[(p + u) * RS + q + 4 * sg]);
-                row[4 * sg] = v.x; row[4 * sg + 1] = v.y; row[4 * sg + 2] = v.z; row[4 * sg + 3] = v.w;
-            }
-#pragma unroll
-            for (int v = 0; v < K; ++v) {
-                const float hv = a.hcorr[u * K + v];
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    acc[k] = EXACT ? acc[k] + hv * row[k + v] : __builtin_fmaf(hv, row[k + v], acc[k]);
-            }
-        }
-        float gv[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) gv[k] = EXACT ? (-acc[k]) / a.sigma2 : (-acc[k]) * a.inv_sigma2;
-        const size_t e0 = (size_t)c * HW + (size_t)i * W + j;   // element index within the chain
-        const size_t o = (size_t)b * a.C * HW + e0;
-        const bool full = (W & 3) == 0;                          // whole aligned quad in range
-        if (a.Y) {
-            float z[4];
-            if (full) {
-                normal_quad(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)(e0 >> 2), z);
-            } else {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    z[k] = normal_elem(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint64_t)(e0 + k));
-            }
-            if (full) {
-                const float4 xv = *reinterpret_cast<const float4*>(a.X + o);
-                const float xk[4] = {xv.x, xv.y, xv.z, xv.w};
-                float yv[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) yv[k] = (xk[k] + a.c1 * gv[k]) + a.c2 * z[k];
-                *reinterpret_cast<float4*>(a.Y + o) = make_float4(yv[0], yv[1], yv[2], yv[3]);
-            } else {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (j + k < W) a.Y[o + k] = (a.X[o + k] + a.c1 * gv[k]) + a.c2 * z[k];
-            }
-        } else if (full) {
-            *reinterpret_cast<float4*>(a.g + o) = make_float4(gv[0], gv[1], gv[2], gv[3]);
-        } else {
+        for (int v = 0; v < K; ++v) {
+            const float hv = h[u * K + v];
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (j + k < W) a.g[o + k] = gv[k];
+                acc[m][k] = EXACT ? acc[m][k] + hv * row[k + v] : __builtin_fmaf(hv, row[k + v], acc[m][k]);
+        }
+    }
+}
+
+template <int SEG>
+__device__ __forceinline__ void bl_load_row(const float* p, float (&row)[SEG * 4]) {
+#pragma unroll
+    for (int sg = 0; sg < SEG; ++sg) {
+        const float4 v = *reinterpret_cast<const float4*>(p + 4 * sg);
+        row[4 * sg] = v.x; row[4 * sg + 1] = v.y; row[4 * sg + 2] = v.z; row[4 * sg + 3] = v.w;
+    }
+}
+
+// One workgroup per (plane, tile), 1-D grid; three resident per CU for l <= 4 (168 VGPRs, 47 KB of LDS).
+// (A persistent variant that DMA'd the next tile into a second buffer during the passes measured slower:
+// two workgroups per CU hide less than three)
+template <bool EXACT, int L>
+__global__ void __launch_bounds__(BL_THREADS, (L <= 4 ? 3 : 1)) blur_grad_kernel(const BlurArgs a) {
+    constexpr int K = 2 * L + 1;
+    constexpr int MR = bl_mr(L);
+    constexpr int RQ = (BL_TW + 2 * L + 3) / 4, RB = (BL_TH + 2 * L + MR - 1) / MR;   // r pass: strips x row blocks
+    constexpr int XH = BL_TH + 4 * L, XW = BL_TW + 4 * L, XQ = XW / 4;                 // staged x (XW % 4 == 0)
+    constexpr int XHA = RB * MR + 2 * L;              // rows the r pass may read (last block: rows past RH unused)
+    constexpr int RHA = RB * MR;
+    // x rows unpadded (XS == XW: the staged tile is one contiguous array, so LDS-DMA rows land back to
+    // back); + 8 floats: the last strip's row segment may run up to 6 floats past the last row
+    constexpr int XS = XW, RS = ((BL_TW + 2 * L + 3) & ~3) + 4;
+    constexpr int SEG = (4 + 2 * L + 3) / 4;                                        // float4 reads per row segment
+    constexpr int TQ = BL_TW / 4, TB = BL_TH / BL_MG;
+    constexpr int NXI = (XH * XQ + BL_THREADS - 1) / BL_THREADS;                     // staging chunks per thread
+    static_assert(TQ * TB == BL_THREADS, "A^T r pass: one block per thread");
+    __shared__ __attribute__((aligned(16))) float xs[XHA * XS + 8];
+    __shared__ __attribute__((aligned(16))) float rs[RHA * RS];
+    const int H = a.H, W = a.W;
+    const size_t HW = (size_t)H * W;
+    const bool vec = (W & 3) == 0;
+    const bool dma = (L & 1) == 0 && vec;   // even l on a 4-aligned width: every staging chunk is one aligned 16-B run
+    const int per_plane = a.tiles_x * a.tiles_y;
+    const long long step = (a.d_step ? *a.d_step : 0LL) + a.off;
+    // circular index without loops: one correction covers every offset an output uses when 2l <= n; tiny
+    // planes (and the unused rows past a partial tile) take the exact modulo
+    auto wrap = [](int v, int n) {
+        if ((unsigned)v < (unsigned)n) return v;
+        const int r = v + (v < 0 ? n : -n);
+        if ((unsigned)r < (unsigned)n) return r;
+        const int m = v % n;
+        return m < 0 ? m + n : m;
+    };
+    struct Tile { int plane, b, c, i0, j0; };
+    auto tile_of = [&](int id) {
+        Tile tl;
+        tl.plane = id / per_plane;
+        const int r = id - tl.plane * per_plane, ty = r / a.tiles_x, tx = r - ty * a.tiles_x;
+        tl.b = tl.plane / a.C; tl.c = tl.plane - tl.b * a.C;
+        tl.i0 = ty * BL_TH; tl.j0 = tx * BL_TW;
+        return tl;
+    };
+    const int t = threadIdx.x;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    // r pass geometry: 4-column x MR-row blocks of rows i0-l .. i0+TH+l-1, cols j0-l .. j0+TW+l-1
+    const bool rblk = t < RQ * RB;
+    const int rq = t % RQ, rb = t / RQ;
+    const int q = 4 * rq, p0 = rb * MR;
+    float yv[MR][4];
+    // the observation under this thread's r block (registers)
+    auto load_y = [&](const Tile& tl) {
+        if (!rblk) return;
+        const float* yp = a.y + (size_t)tl.b * a.y_cs + (size_t)tl.c * HW;
+        const int gj = tl.j0 - L + q;
+        const bool yvec = (L & 3) == 0 && vec && gj >= 0 && gj + 3 < W;
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+            yv[m][0] = yv[m][1] = yv[m][2] = yv[m][3] = 0.f;
+#ifdef PSGLA_ABL_BLUR_NOLOAD
+            if (false) {
+#else
+            if (p0 + m < BL_TH + 2 * L) {
+#endif
+                const float* yrow = yp + (size_t)wrap(tl.i0 - L + p0 + m, H) * W;
+                if (yvec) {
+                    const float4 v = ld4(yrow + gj);
+                    yv[m][0] = v.x; yv[m][1] = v.y; yv[m][2] = v.z; yv[m][3] = v.w;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (q + k < BL_TW + 2 * L) yv[m][k] = yrow[wrap(gj + k, W)];
+                }
+            }
+        }
+    };
+    // x on rows i0-2l .. i0+TH+2l-1, cols j0-2l .. j0+TW+2l-1 (circular padding applied twice), in
+    // 4-column chunks: chunk n of the tile -> buf[4n].  LDS-DMA (no registers, all in flight at once) or,
+    // for odd l / widths not a multiple of 4, element loads through registers.
+    auto stage_x = [&](const Tile& tl, float* buf) {
+        const float* xp = a.X + (size_t)tl.plane * HW;
+#ifndef PSGLA_ABL_BLUR_NOLOAD
+        if (dma) {
+#pragma unroll
+            for (int it = 0; it < NXI; ++it) {
+                const int n = it * BL_THREADS + t;
+                if (n < XH * XQ) {
+                    const int p = n / XQ, qq = n - p * XQ;
+                    glds16(xp + (size_t)wrap(tl.i0 - 2 * L + p, H) * W + wrap(tl.j0 - 2 * L + 4 * qq, W),
+                           &buf[4 * (it * BL_THREADS + 64 * wv)]);
+                }
+            }
+            return;
+        }
+#endif
+        for (int n = t; n < XH * XQ; n += BL_THREADS) {
+            const int p = n / XQ, qq = n - p * XQ;
+            const float* rowp = xp + (size_t)wrap(tl.i0 - 2 * L + p, H) * W;
+            const int gj = tl.j0 - 2 * L + 4 * qq;
+            float4 v;
+#ifdef PSGLA_ABL_BLUR_NOLOAD
+            v = make_float4(0.f, 0.f, 0.f, (float)gj);   // diagnostic timing build only
+#else
+            v.x = rowp[wrap(gj, W)]; v.y = rowp[wrap(gj + 1, W)];
+            v.z = rowp[wrap(gj + 2, W)]; v.w = rowp[wrap(gj + 3, W)];
+#endif
+            *reinterpret_cast<float4*>(&buf[4 * n]) = v;
+        }
+    };
+
+    const Tile tl = tile_of(blockIdx.x);
+    load_y(tl);                              // y first: it has landed by the time the tile has
+    stage_x(tl, xs);
+    wait_vm0();                              // this wave's x chunks and y landed
+    __syncthreads();
+    {
+        const float* xb = xs;
+        // r = A x - y
+        if (rblk) {
+            float acc[MR][4];
+#pragma unroll
+            for (int m = 0; m < MR; ++m) acc[m][0] = acc[m][1] = acc[m][2] = acc[m][3] = 0.f;
+#pragma unroll
+            for (int ir = 0; ir < MR + 2 * L; ++ir) {
+                float row[SEG * 4];
+                bl_load_row<SEG>(&xb[(p0 + ir) * XS + q], row);
+#ifndef PSGLA_ABL_BLUR_NOR
+                bl_row_accumulate<EXACT, K, MR, SEG>(a.hconv, row, ir, acc);
+#else
+                acc[0][ir & 3] += row[0];
+#endif
+            }
+#pragma unroll
+            for (int m = 0; m < MR; ++m)
+                *reinterpret_cast<float4*>(&rs[(p0 + m) * RS + q]) =
+                    make_float4(acc[m][0] - yv[m][0], acc[m][1] - yv[m][1], acc[m][2] - yv[m][2], acc[m][3] - yv[m][3]);
+        }
+        __syncthreads();
+        // g = -(A^T r) / sigma2 on the tile (+ the fused Langevin update): 4-column x 4-row blocks
+        const int gq = 4 * (t % TQ), gp0 = BL_MG * (t / TQ);
+        const int j = tl.j0 + gq;
+        if (j < W && tl.i0 + gp0 < H) {
+            float acc[BL_MG][4];
+#pragma unroll
+            for (int m = 0; m < BL_MG; ++m) acc[m][0] = acc[m][1] = acc[m][2] = acc[m][3] = 0.f;
+#pragma unroll
+            for (int ir = 0; ir < BL_MG + 2 * L; ++ir) {
+                float row[SEG * 4];
+                bl_load_row<SEG>(&rs[(gp0 + ir) * RS + gq], row);
+#ifndef PSGLA_ABL_BLUR_NOG
+                bl_row_accumulate<EXACT, K, BL_MG, SEG>(a.hcorr, row, ir, acc);
+#else
+                acc[0][ir & 3] += row[0];
+#endif
+            }
+#pragma unroll
+            for (int m = 0; m < BL_MG; ++m) {
+                const int i = tl.i0 + gp0 + m;
+                if (i >= H) break;
+                float gv[4];
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) gv[kk] = EXACT ? (-acc[m][kk]) / a.sigma2 : (-acc[m][kk]) * a.inv_sigma2;
+                const size_t e0 = (size_t)tl.c * HW + (size_t)i * W + j;   // element index within the chain
+                const size_t o = (size_t)tl.b * a.C * HW + e0;
+                if (a.Y) {
+                    float z[4];
+                    if (vec) {
+                        normal_quad(a.seed, (uint32_t)(a.chain0 + tl.b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)(e0 >> 2), z);
+                    } else {
+#pragma unroll
+                        for (int kk = 0; kk < 4; ++kk)
+                            z[kk] = normal_elem(a.seed, (uint32_t)(a.chain0 + tl.b), (uint32_t)step, TAG_LANGEVIN,
+                                                (uint64_t)(e0 + kk));
+                    }
+                    // X of the tile from the staged copy (the same values as a.X)
+                    const float* xr = &xb[(gp0 + m + 2 * L) * XS + gq + 2 * L];
+                    float yo[4];
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) yo[kk] = (xr[kk] + a.c1 * gv[kk]) + a.c2 * z[kk];
+                    if (vec) {
+                        *reinterpret_cast<float4*>(a.Y + o) = make_float4(yo[0], yo[1], yo[2], yo[3]);
+                    } else {
+#pragma unroll
+                        for (int kk = 0; kk < 4; ++kk)
+                            if (j + kk < W) a.Y[o + kk] = yo[kk];
+                    }
+                } else if (vec) {
+                    *reinterpret_cast<float4*>(a.g + o) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+                } else {
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk)
+                        if (j + kk < W) a.g[o + kk] = gv[kk];
+                }
+            }
         }
     }
 }
@@ -3639,8 +3767,10 @@ int psgla_blur_grad(const float* X, const float* y, int64_t y_chain_stride, cons
     a.c1 = c1; a.c2 = c2; a.seed = seed; a.chain0 = chain0; a.d_step = (const long long*)d_step;
     a.off = step_offset;
     a.tiles_x = (W + BL_TW - 1) / BL_TW;
-    const int tiles_y = (H + BL_TH - 1) / BL_TH;
-    const dim3 grid(a.tiles_x * tiles_y, B * C);
+    a.tiles_y = (H + BL_TH - 1) / BL_TH;
+    const long long ntiles = (long long)a.tiles_x * a.tiles_y * B * C;
+    if (ntiles > (1LL << 30)) return fail(0, "psgla_blur_grad: too many tiles");
+    const dim3 grid((unsigned)ntiles);
     if (exact) launch_blur<true>(a, l, grid, (hipStream_t)stream);
     else launch_blur<false>(a, l, grid, (hipStream_t)stream);
     return launch_check("blur_grad");

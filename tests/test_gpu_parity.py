@@ -498,6 +498,25 @@ def test_blur_grad_matches_reference_closure(B, H, W, l, bt, exact):
     assert err <= BLUR_TOL * ref.abs().max().item(), err
 
 
+@pytest.mark.parametrize("B,H,W,l", [(2, 40, 52, 4), (1, 37, 29, 4), (2, 70, 130, 2), (1, 16, 16, 0),
+                                     (1, 45, 70, 3), (1, 50, 44, 8), (1, 130, 200, 4), (1, 33, 40, 6)])
+def test_blur_grad_exact_bitwise_vs_tap_order_oracle(B, H, W, l):
+    """Exact mode sums every output's (2l+1)^2 products in (row, column) tap order with IEEE
+    multiply / add / divide: bit-identical to oracle.blur_grad_tap_order on odd widths, partial
+    tiles, several tiles per plane, odd and even l (LDS-DMA and register staging)."""
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    g = torch.Generator().manual_seed(H * W + l)
+    x = torch.rand((B, 3, H, W), generator=g)
+    y = torch.rand((B, 3, H, W), generator=g)
+    h_ = orc.blur_kernel(l, "gaussian").astype(np.float32)
+    hconv = np.flip(h_).copy()
+    s2 = float(np.float32((1 / 255.0) ** 2))
+    got = K.blur_grad(x.to(DEV), y.to(DEV), torch.from_numpy(hconv), torch.from_numpy(h_), l, s2, exact=True)
+    torch.cuda.synchronize()
+    want = orc.blur_grad_tap_order(x.numpy(), y.numpy(), hconv, h_, l, s2)
+    np.testing.assert_array_equal(got.cpu().numpy(), want)
+
+
 def test_blur_langevin_fused_equals_grad_then_update():
     """The fused stencil + Langevin kernel == blur_grad followed by langevin_update (same noise)."""
     from psgla_for_posterior_sampling_amd import hip_ops as K

@@ -120,6 +120,23 @@ def test_psgla_deblur(bt):
     _chk(out, fx)
 
 
+@pytest.mark.parametrize("bt,l", [("uniform", 4), ("gaussian", 2), ("uniform", 0)])
+def test_blur_tap_order_restatement_matches_reference_closure(bt, l):
+    """oracle.blur_grad_tap_order (the stencil's summation order, which pins the HIP kernel bit for
+    bit) computes the reference closure -AT(A x - y) / sigma2 (sampling_images.py:329-338, here
+    through the fixture's observation y) to fp32 rounding: |d| <= 2e-5 max|g|."""
+    fx = load(f"psgla_deblur_{bt}")
+    x = torch.from_numpy(fx["x"])
+    dg, y, _ = orc.deblurring_problem(x, seed_ip=0, l=l, blur_type=bt)
+    xs = (x + 0.05 * torch.randn(x.shape, generator=torch.Generator().manual_seed(1))).float()
+    ref = dg(xs).numpy()
+    h_ = orc.blur_kernel(l, bt)
+    got = orc.blur_grad_tap_order(xs.numpy(), y.numpy(), np.flip(h_).astype(np.float32),
+                                  h_.astype(np.float32), l, float(np.float32((1 / 255.0) ** 2)))
+    assert got.dtype == np.float32
+    assert np.abs(got - ref).max() <= 2e-5 * np.abs(ref).max()
+
+
 def test_pnpula_inpaint_clamp():
     fx = load("pnpula_inpaint_clamp")
     seed, n, ni, nm, alpha, lam, s1, delta = fx["meta"]
