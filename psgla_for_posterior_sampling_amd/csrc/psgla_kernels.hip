@@ -2771,6 +2771,41 @@ __device__ __forceinline__ void bl_row_accumulate(const float* __restrict__ h, c
     }
 }
 
+#ifdef PSGLA_BLUR_PK
+// Experimental (build flag; bit-identical, measured in DESIGN section 3.3: the extra row copy costs
+// the registers of a third workgroup per CU, so it does not pay).  Packed form: acc pairs (columns k, k+1) and row pairs; {row[v], row[v+1]} for odd v comes from a copy of
+// the row shifted by one (register pairs must be even-aligned).  Same roundings, same order.
+typedef float bl_f2 __attribute__((ext_vector_type(2)));
+template <bool EXACT, int K, int M, int SEG>
+__device__ __forceinline__ void bl_row_accumulate_pk(const float* __restrict__ h, const float (&row)[SEG * 4], int ir,
+                                                     bl_f2 (&acc)[M][2]) {
+    bl_f2 re[SEG * 2], ro[SEG * 2 - 1];
+#pragma unroll
+    for (int j = 0; j < SEG * 2; ++j) { re[j].x = row[2 * j]; re[j].y = row[2 * j + 1]; }
+#pragma unroll
+    for (int j = 0; j < SEG * 2 - 1; ++j) { ro[j].x = row[2 * j + 1]; ro[j].y = row[2 * j + 2]; }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        const int u = ir - m;
+        if (u < 0 || u >= K) continue;
+#pragma unroll
+        for (int v = 0; v < K; ++v) {
+            const float hv = h[u * K + v];
+            const bl_f2 h2 = {hv, hv};
+            const bl_f2 p0 = (v & 1) ? ro[(v - 1) / 2] : re[v / 2];
+            const bl_f2 p1 = (v & 1) ? ro[(v + 1) / 2] : re[v / 2 + 1];
+            if (EXACT) {
+                acc[m][0] = acc[m][0] + h2 * p0;
+                acc[m][1] = acc[m][1] + h2 * p1;
+            } else {
+                acc[m][0] = __builtin_elementwise_fma(h2, p0, acc[m][0]);
+                acc[m][1] = __builtin_elementwise_fma(h2, p1, acc[m][1]);
+            }
+        }
+    }
+}
+#endif
+
 template <int SEG>
 __device__ __forceinline__ void bl_load_row(const float* p, float (&row)[SEG * 4]) {
 #pragma unroll
@@ -2783,8 +2818,11 @@ __device__ __forceinline__ void bl_load_row(const float* p, float (&row)[SEG * 4
 // One workgroup per (plane, tile), 1-D grid; three resident per CU for l <= 4 (168 VGPRs, 47 KB of LDS).
 // (A persistent variant that DMA'd the next tile into a second buffer during the passes measured slower:
 // two workgroups per CU hide less than three)
+#ifndef PSGLA_BLUR_WPE
+#define PSGLA_BLUR_WPE 3
+#endif
 template <bool EXACT, int L>
-__global__ void __launch_bounds__(BL_THREADS, (L <= 4 ? 3 : 1)) blur_grad_kernel(const BlurArgs a) {
+__global__ void __launch_bounds__(BL_THREADS, (L <= 4 ? PSGLA_BLUR_WPE : 1)) blur_grad_kernel(const BlurArgs a) {
     constexpr int K = 2 * L + 1;
     constexpr int MR = bl_mr(L);
     constexpr int RQ = (BL_TW + 2 * L + 3) / 4, RB = (BL_TH + 2 * L + MR - 1) / MR;   // r pass: strips x row blocks
@@ -2891,7 +2929,20 @@ __global__ void __launch_bounds__(BL_THREADS, (L <= 4 ? 3 : 1)) blur_grad_kernel
         }
     };
 
+#ifndef PSGLA_BLUR_NOXCD
+    // workgroups are dealt round-robin to the 8 XCDs: give each XCD a contiguous run of tiles so the
+    // halo rows / columns a tile shares with its neighbours are re-read from the same L2 (-5 %; the
+    // loads-and-stores floor 44 -> 31 us)
+    int tid;
+    {
+        const int ntiles = per_plane * a.B * a.C, bid = blockIdx.x;
+        const int xcd = bid & 7, k = bid >> 3, qt = ntiles >> 3, rt = ntiles & 7;
+        tid = xcd * qt + min(xcd, rt) + k;
+    }
+    const Tile tl = tile_of(tid);
+#else
     const Tile tl = tile_of(blockIdx.x);
+#endif
     load_y(tl);                              // y first: it has landed by the time the tile has
     stage_x(tl, xs);
     wait_vm0();                              // this wave's x chunks and y landed
@@ -2901,6 +2952,21 @@ __global__ void __launch_bounds__(BL_THREADS, (L <= 4 ? 3 : 1)) blur_grad_kernel
         // r = A x - y
         if (rblk) {
             float acc[MR][4];
+#ifdef PSGLA_BLUR_PK
+            bl_f2 acc2[MR][2];
+#pragma unroll
+            for (int m = 0; m < MR; ++m) acc2[m][0] = acc2[m][1] = bl_f2{0.f, 0.f};
+#pragma unroll
+            for (int ir = 0; ir < MR + 2 * L; ++ir) {
+                float row[SEG * 4];
+                bl_load_row<SEG>(&xb[(p0 + ir) * XS + q], row);
+                bl_row_accumulate_pk<EXACT, K, MR, SEG>(a.hconv, row, ir, acc2);
+            }
+#pragma unroll
+            for (int m = 0; m < MR; ++m) {
+                acc[m][0] = acc2[m][0].x; acc[m][1] = acc2[m][0].y; acc[m][2] = acc2[m][1].x; acc[m][3] = acc2[m][1].y;
+            }
+#else
 #pragma unroll
             for (int m = 0; m < MR; ++m) acc[m][0] = acc[m][1] = acc[m][2] = acc[m][3] = 0.f;
 #pragma unroll
@@ -2913,6 +2979,7 @@ __global__ void __launch_bounds__(BL_THREADS, (L <= 4 ? 3 : 1)) blur_grad_kernel
                 acc[0][ir & 3] += row[0];
 #endif
             }
+#endif
 #pragma unroll
             for (int m = 0; m < MR; ++m)
                 *reinterpret_cast<float4*>(&rs[(p0 + m) * RS + q]) =
@@ -2924,6 +2991,21 @@ __global__ void __launch_bounds__(BL_THREADS, (L <= 4 ? 3 : 1)) blur_grad_kernel
         const int j = tl.j0 + gq;
         if (j < W && tl.i0 + gp0 < H) {
             float acc[BL_MG][4];
+#ifdef PSGLA_BLUR_PK
+            bl_f2 acc2[BL_MG][2];
+#pragma unroll
+            for (int m = 0; m < BL_MG; ++m) acc2[m][0] = acc2[m][1] = bl_f2{0.f, 0.f};
+#pragma unroll
+            for (int ir = 0; ir < BL_MG + 2 * L; ++ir) {
+                float row[SEG * 4];
+                bl_load_row<SEG>(&rs[(gp0 + ir) * RS + gq], row);
+                bl_row_accumulate_pk<EXACT, K, BL_MG, SEG>(a.hcorr, row, ir, acc2);
+            }
+#pragma unroll
+            for (int m = 0; m < BL_MG; ++m) {
+                acc[m][0] = acc2[m][0].x; acc[m][1] = acc2[m][0].y; acc[m][2] = acc2[m][1].x; acc[m][3] = acc2[m][1].y;
+            }
+#else
 #pragma unroll
             for (int m = 0; m < BL_MG; ++m) acc[m][0] = acc[m][1] = acc[m][2] = acc[m][3] = 0.f;
 #pragma unroll
@@ -2936,6 +3018,7 @@ __global__ void __launch_bounds__(BL_THREADS, (L <= 4 ? 3 : 1)) blur_grad_kernel
                 acc[0][ir & 3] += row[0];
 #endif
             }
+#endif
 #pragma unroll
             for (int m = 0; m < BL_MG; ++m) {
                 const int i = tl.i0 + gp0 + m;
