@@ -243,6 +243,10 @@ int psgla_blur_grad(const float* X, const float* y, int64_t y_chain_stride, cons
                     int32_t l, float* g, float* Y, int32_t B, int32_t C, int32_t H, int32_t W, float sigma2,
                     float c1, float c2, uint64_t seed, int32_t chain0, const int64_t* d_step, int64_t step_offset,
                     int32_t exact, void* stream);
+/* Fast mode (exact = 0) runs rank-1 taps (the reference's h^T h kernels) as separable row / column passes
+ * (results within fp32 rounding of the 2-D stencil); enable = 0 keeps every call on the 2-D stencil
+ * (process-wide switch, for A/B and tests; default 1). */
+int psgla_blur_set_separable(int32_t enable);
 /* *d_step += 1 (one thread) */
 int psgla_advance_step(int64_t* d_step, void* stream);
 

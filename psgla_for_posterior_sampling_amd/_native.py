@@ -82,6 +82,7 @@ _SIGNATURES = {
                                    c_vp]),
     "psgla_blur_grad": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32,
                                 c_f, c_f, c_f, c_u64, c_i32, c_vp, c_i64, c_i32, c_vp]),
+    "psgla_blur_set_separable": (c_i32, [c_i32]),
     "psgla_advance_step": (c_i32, [c_vp, c_vp]),
     "psgla_bias_act": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i64, c_i32, c_vp]),
     "psgla_debug_bm_tables": (c_i32, [c_vp, c_vp, c_vp, c_u32, c_u32, c_vp]),

@@ -230,6 +230,12 @@ def blur_grad(X, y, hconv, hcorr, l: int, sigma2: float, out=None, exact: bool =
     return out
 
 
+def blur_set_separable(enable: bool) -> None:
+    """Fast-mode rank-1 taps take the separable row / column passes (default) or, with False, the
+    2-D stencil (process-wide; A/B and tests)."""
+    N.check(N.lib().psgla_blur_set_separable(int(bool(enable))), "psgla_blur_set_separable")
+
+
 def blur_langevin(X, y, hconv, hcorr, l: int, sigma2: float, c1: float, c2: float, seed: int, chain0: int,
                   step: int, out=None, exact: bool = False, d_step: torch.Tensor | None = None):
     """Y = (X + c1 g(X)) + c2 Z with the deblurring g fused (restoration_algorithms.py:232-236)."""

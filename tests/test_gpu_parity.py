@@ -517,6 +517,36 @@ def test_blur_grad_exact_bitwise_vs_tap_order_oracle(B, H, W, l):
     np.testing.assert_array_equal(got.cpu().numpy(), want)
 
 
+def test_blur_fast_separable_path():
+    """Fast mode runs the reference's rank-1 (h^T h) taps as separable row / column passes: within fp32
+    rounding of the 2-D stencil (3e-6 of max|g| measured on a real deblurring observation, where A x - y
+    cancels; bound 1e-5, half the 2e-5 contract against the reference closure, which it also meets);
+    taps that are not rank 1 stay on the 2-D stencil (bitwise equal to it)."""
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    xs, y, ref = _blur_case(2, 70, 130, 4, "gaussian", seed=11)
+    h_ = orc.blur_kernel(4, "gaussian")
+    hconv = torch.from_numpy(np.copy(np.flip(h_))).float()
+    hcorr = torch.from_numpy(h_).float()
+    s2 = float(np.float32((1 / 255.0) ** 2))
+    X, yd = xs.to(DEV), y.to(DEV)
+    try:
+        g_sep = K.blur_grad(X, yd, hconv, hcorr, 4, s2).cpu()
+        K.blur_set_separable(False)
+        g_2d = K.blur_grad(X, yd, hconv, hcorr, 4, s2).cpu()
+        assert (g_sep - g_2d).abs().max().item() <= 1e-5 * g_2d.abs().max().item()
+        assert (g_sep - ref).abs().max().item() <= BLUR_TOL * ref.abs().max().item()
+        # a full-rank tap set: the 2-D stencil either way
+        hr = torch.rand((9, 9), generator=torch.Generator().manual_seed(3))
+        hr = hr / hr.sum()
+        g_a = K.blur_grad(X, yd, hr, hr.t().contiguous(), 4, s2).cpu()
+        K.blur_set_separable(True)
+        g_b = K.blur_grad(X, yd, hr, hr.t().contiguous(), 4, s2).cpu()
+        torch.cuda.synchronize()
+        assert torch.equal(g_a, g_b)
+    finally:
+        K.blur_set_separable(True)
+
+
 def test_blur_langevin_fused_equals_grad_then_update():
     """The fused stencil + Langevin kernel == blur_grad followed by langevin_update (same noise)."""
     from psgla_for_posterior_sampling_amd import hip_ops as K

@@ -26,8 +26,10 @@ def taps(l):
     return torch.from_numpy(np.flip(h_).copy()).float(), torch.from_numpy(h_).float()
 
 
-def run(tag):
+def run(tag, no_sep=False):
     from psgla_for_posterior_sampling_amd import hip_ops as K
+    if no_sep:
+        K.blur_set_separable(False)
     dev = "cuda"
     out = {}
     g = torch.Generator().manual_seed(0)
@@ -78,7 +80,7 @@ def compare(t1, t2):
         if not same:
             bad += 1
             d = (a[k] - b[k]).abs().max().item()
-            print("DIFF", k, d, a[k].abs().max().item())
+            print("DIFF", k, f"max|d| {d:.3e}  max|a| {a[k].abs().max().item():.3e}  rel {d / a[k].abs().max().item():.2e}")
     print(f"{len(a) - bad}/{len(a)} outputs bitwise equal")
     return bad
 
@@ -87,7 +89,8 @@ if __name__ == "__main__":
     p = argparse.ArgumentParser()
     p.add_argument("--tag")
     p.add_argument("--compare", nargs=2)
+    p.add_argument("--no-sep", action="store_true", help="fast mode on the 2-D stencil (psgla_blur_set_separable(0))")
     a = p.parse_args()
     if a.compare:
         sys.exit(1 if compare(*a.compare) else 0)
-    run(a.tag)
+    run(a.tag, a.no_sep)
