@@ -629,14 +629,24 @@ typedef float v4f_t __attribute__((ext_vector_type(4)));
 // Issued as inline asm: the compiler does not track these loads, so it cannot insert a
 // conservative vmcnt(0) before unrelated LDS accesses -- the waves wait with counted
 // s_waitcnt vmcnt(N) themselves (vector-memory operations retire in issue order).
+// PSGLA_DMA_AUX: cache-policy bits of the LDS-DMA loads (diagnostic A/B builds; default none)
+#if defined(PSGLA_DMA_POL) && PSGLA_DMA_POL == 1
+#define PSGLA_DMA_AUX " nt"
+#elif defined(PSGLA_DMA_POL) && PSGLA_DMA_POL == 2
+#define PSGLA_DMA_AUX " sc1"
+#elif defined(PSGLA_DMA_POL) && PSGLA_DMA_POL == 3
+#define PSGLA_DMA_AUX " sc0 sc1 nt"
+#else
+#define PSGLA_DMA_AUX ""
+#endif
 __device__ __forceinline__ void glds16(const void* src, void* dst) {
     const unsigned off = (unsigned)(size_t)(lptr_t)dst;
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" PSGLA_DMA_AUX
                  :: "v"(src), "s"(off) : "memory", "m0");
 }
 __device__ __forceinline__ void glds4(const void* src, void* dst) {
     const unsigned off = (unsigned)(size_t)(lptr_t)dst;
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off"
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" PSGLA_DMA_AUX
                  :: "v"(src), "s"(off) : "memory", "m0");
 }
 // SGPR-base forms (per-wave pipeline kernel): global_* with a wave-uniform 64-bit base in SGPRs (saddr) and
