@@ -484,7 +484,8 @@ BLUR_TOL = 2e-5
 
 
 @pytest.mark.parametrize("B,H,W,l,bt", [(2, 40, 52, 4, "uniform"), (1, 37, 29, 4, "gaussian"),
-                                        (2, 70, 130, 2, "uniform"), (1, 16, 16, 0, "uniform")])
+                                        (2, 70, 130, 2, "uniform"), (1, 16, 16, 0, "uniform"),
+                                        (1, 45, 71, 3, "gaussian"), (1, 130, 200, 5, "uniform")])
 @pytest.mark.parametrize("exact", [True, False])
 def test_blur_grad_matches_reference_closure(B, H, W, l, bt, exact):
     from psgla_for_posterior_sampling_amd import hip_ops as K
