@@ -572,7 +572,7 @@ __global__ void __launch_bounds__(TV_THREADS) tv_finalise_kernel(const TvArgs a)
         if (threadIdx.x == 0) {
             *a.arrive = 0;
             if (a.fresh_dev) *a.fresh_dev = 0;
-            if (a.advance_step && a.d_step) *a.d_step = *a.d_step + 1;
+            if (a.advance_step && a.d_step) *a.d_step = step - a.step_offset + 1;   // the value read at the start: no dependent load
         }
     }
 }
@@ -1783,7 +1783,7 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     if (threadIdx.x == 0) {
         *a.arrive = 0;
         if (a.fresh_dev) *a.fresh_dev = 0;
-        if (a.advance_step && a.d_step) *a.d_step = *a.d_step + 1;
+        if (a.advance_step && a.d_step) *a.d_step = *a.d_step + 1;   // (re-read: the start-of-kernel value measured +0.5 % here)
     }
 }
 
@@ -2090,19 +2090,32 @@ __global__ void __launch_bounds__(TV_THREADS) tv_tile_kernel(const TvArgs a) {
         const int band = k - (k / T) * T;
         if (plane < P) sb_tile<EXACT, ALPHA1, R>(a, sh, plane, band, a.n_tv, true, step, fresh);
     }
+#ifdef PSGLA_ABL_TILE_NOFIN
+    return;              // diagnostic timing build only: no arrival / finalisation
+#endif
     if (!a.fin_inline) return;
     // ---- step finalisation by the last workgroup to arrive (as tv_stream_kernel) ----
+#ifndef PSGLA_ABL_TILE_NOWAIT
     wait_vm0();
+#endif
     __syncthreads();
     if (threadIdx.x == 0) {
+#ifndef PSGLA_ABL_TILE_NOREL
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
         const int old = __hip_atomic_fetch_add(a.arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sh.s_flag = (old == (int)gridDim.x - 1) ? 1 : 0;
+#ifndef PSGLA_ABL_TILE_NOACQ
         if (sh.s_flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
     }
     wait_vm0();
     __syncthreads();
     if (!sh.s_flag) return;
+#ifdef PSGLA_ABL_TILE_NOLAST
+    if (threadIdx.x == 0) { *a.arrive = 0; if (a.advance_step && a.d_step) *a.d_step = step - a.step_offset + 1; }
+    return;              // diagnostic timing build only
+#endif
     const int G = a.B;
     for (int g = threadIdx.x; g < G; g += blockDim.x) sh.s_stop[g] = 0;
     __syncthreads();
@@ -2141,7 +2154,7 @@ __global__ void __launch_bounds__(TV_THREADS) tv_tile_kernel(const TvArgs a) {
     if (threadIdx.x == 0) {
         *a.arrive = 0;
         if (a.fresh_dev) *a.fresh_dev = 0;
-        if (a.advance_step && a.d_step) *a.d_step = *a.d_step + 1;
+        if (a.advance_step && a.d_step) *a.d_step = step - a.step_offset + 1;   // the value read at the start: no dependent load
     }
 }
 
@@ -2662,7 +2675,7 @@ __global__ void __launch_bounds__(WV_THREADS) tv_wave_kernel(const TvArgs a) {
     if (threadIdx.x == 0) {
         *a.arrive = 0;
         if (a.fresh_dev) *a.fresh_dev = 0;
-        if (a.advance_step && a.d_step) *a.d_step = *a.d_step + 1;
+        if (a.advance_step && a.d_step) *a.d_step = step - a.step_offset + 1;   // the value read at the start: no dependent load
     }
 }
 
