@@ -2100,12 +2100,19 @@ __global__ void __launch_bounds__(TV_THREADS) tv_tile_kernel(const TvArgs a) {
 #endif
     __syncthreads();
     if (threadIdx.x == 0) {
-#ifndef PSGLA_ABL_TILE_NOREL
+#ifdef PSGLA_TILE_FENCED
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
+        // Without fences: every output of this kernel is an sc1 (write-through) store and every rel-err sum
+        // an agent-scope atomic; each wave waited vmcnt(0) before the barrier above, one lane per workgroup
+        // adds to the arrival counter, and the workgroup whose add returns the last count reads the sums by
+        // agent atomics (MI355X_MICROARCH.md: "8-B agent atomics both sides" with its hand-off row 1; a
+        // release + acquire pair cost 1.1 us per step here).  Nothing else this launch wrote is read by it
+        // (the rare redo reads the step's inputs, written by the previous launch).
         const int old = __hip_atomic_fetch_add(a.arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sh.s_flag = (old == (int)gridDim.x - 1) ? 1 : 0;
-#ifndef PSGLA_ABL_TILE_NOACQ
+#ifdef PSGLA_TILE_FENCED
         if (sh.s_flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #endif
     }
@@ -2122,8 +2129,12 @@ __global__ void __launch_bounds__(TV_THREADS) tv_tile_kernel(const TvArgs a) {
     for (int i = threadIdx.x; i < G * MAXIT; i += blockDim.x) {
         const int g = i / MAXIT, t = i - g * MAXIT;
         if (t >= trk_lo(a) && t <= trk_hi(a) && t < a.n_tv) {
-            const double nd = a.norms[((size_t)g * a.n_tv + t) * 2];
-            const double nn = a.norms[((size_t)g * a.n_tv + t) * 2 + 1];
+            // read by agent-scope atomics (+0.0, returning), as they were written: 8-B agent atomics on both
+            // sides of the hand-off, performed where the producers' adds were
+            const double nd = __hip_atomic_fetch_add(&a.norms[((size_t)g * a.n_tv + t) * 2], 0.0, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+            const double nn = __hip_atomic_fetch_add(&a.norms[((size_t)g * a.n_tv + t) * 2 + 1], 0.0, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
             const float rel = (float)sqrt(nd) / (float)sqrt(nn);
             if (rel < a.tol) atomicOr(&sh.s_stop[g], 1 << t);
         }
