@@ -782,6 +782,37 @@ def test_tile_kernel_equals_stream_kernel_full_size(B):
             assert torch.equal(a, b), f"exact={exact}"
 
 
+@pytest.mark.parametrize("tol", [3e-3, 1e-3])
+def test_tile_kernel_early_stop_handoff_full_size(tol):
+    """The tile kernel's fence-free step hand-off (sc1 stores, rel-err sums as agent atomics read back by
+    the last workgroup's agent atomics) under a tolerance at which deepinv's early stop fires: 40 steps of
+    8 chains at 3 x 256 x 256 bit-identical to the row-streaming kernel (which keeps its release / acquire
+    fences), and different from the same run without early stops (so stops did fire)."""
+    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    B = 8
+    g = torch.Generator(device=DEV).manual_seed(77)
+    xs = torch.rand((B, 3, 256, 256), generator=g, device=DEV)
+    gen = torch.Generator(device=DEV).manual_seed(0)
+    mask2d = (torch.rand((256, 256), generator=gen, device=DEV) > 0.5).to(torch.uint8)
+    y = mask2d.float() * xs + torch.normal(torch.zeros_like(xs), std=(1 / 255.0) * torch.ones_like(xs),
+                                           generator=gen)
+    init = (mask2d.float() * y + (1 - mask2d.float()) * 0.5).contiguous()
+    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
+    outs = {}
+    for variant, t in (("stream", tol), ("tile", tol), ("tile", 1e-5)):
+        eng = FusedTvChains(init, y.contiguous(), mask2d, c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
+                            alpha=1.0, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10, tol=t),
+                            seed=0, n_iter=40, n_inter=10, n_inter_mmse=10, kernel_variant=variant)
+        eng.run(40, graph_steps=10)
+        torch.cuda.synchronize()
+        bm, bm2 = eng.blocks()
+        outs[(variant, t)] = (eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone())
+    for a, b in zip(outs[("stream", tol)], outs[("tile", tol)]):
+        assert torch.equal(a, b)
+    assert not torch.equal(outs[("tile", tol)][3], outs[("tile", 1e-5)][3]), "no early stop fired"
+
+
 @pytest.mark.parametrize("B,H,W,alpha,tol,n_tv", [
     (3, 48, 64, 1.0, 1e-5, 10),      # 3 ranges per plane: halo cuts at both ends
     (2, 100, 64, 1.0, 1e-5, 10),     # 6 ranges per plane
