@@ -76,6 +76,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the batch-1 CPU leg")
     p.add_argument("--cpu-b64-steps", type=int, default=10, help="timed steps of the batch-64 CPU leg (0: skip)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--multi-step", action="store_true",
+                   help="graph segments as one persistent multi-step tile-kernel launch (analysis; DESIGN.md 3.1d)")
     p.add_argument("--pmc-json", default=None, help="PMC summary to report as roofline.traffic (default: the "
                    "committed profile of the dispatched kernel, when it was measured on this workload)")
     return p.parse_args()
@@ -221,7 +223,8 @@ def main():
                         sigma2=float(np.float32(sigma1 ** 2)), alpha=1.0, ths=float(np.float32(s)),
                         tv=K.TvConstants(n_it_max=args.tv_iters), seed=0, n_iter=n_iter + args.kernel_iters,
                         n_inter=n_inter, n_inter_mmse=nm, chain0=c0, exact=args.exact,
-                        stream_wgs=args.stream_wgs, kernel_variant=args.variant)
+                        stream_wgs=args.stream_wgs, kernel_variant=args.variant,
+                        multi_step=args.multi_step)
     # warm-up: eager steps + graph capture + one replay
     eng.step(w_eager)
     eng.capture(gs)
@@ -286,11 +289,14 @@ def main():
     psnr_sum, n_chains = reduce_psnr(blocks, xs, world)
 
     traffic, traffic_info = None, None
-    pmc_json = args.pmc_json or os.path.join(REPO, PMC_PROFILES.get(eng.main_kernel, "none"))
+    # the kernel the timed graphs launch: one persistent launch per graph segment when the tile kernel's
+    # tiles are all resident (tv_tile_multi_kernel), else one launch of main_kernel per step
+    kname = "tv_tile_multi_kernel" if (gs > 1 and eng.multi_step_active) else eng.main_kernel
+    pmc_json = args.pmc_json or os.path.join(REPO, PMC_PROFILES.get(kname, "none"))
     if os.path.exists(pmc_json):
         try:
             pj = json.load(open(pmc_json))
-            if (pj.get("kernel") == eng.main_kernel and pj.get("workload", {}).get("chains_per_gpu") in (None, B)
+            if (pj.get("kernel") == kname and pj.get("workload", {}).get("chains_per_gpu") in (None, B)
                     and pj.get("exact", False) == args.exact
                     and args.tv_iters == 10 and (H, W) == (256, 256)):
                 traffic = pj.get("hbm_bytes_per_launch")
@@ -301,11 +307,12 @@ def main():
             traffic = None
 
     if rank == 0:
-        cpu = None if args.no_cpu else cpu_baseline(args.cpu_seconds, args.cpu_b64_steps)
+        # the CPU baseline is timed at N = 1 only (rank 0 alone on the host); multi-GPU lines carry null
+        cpu = None if (args.no_cpu or world > 1) else cpu_baseline(args.cpu_seconds, args.cpu_b64_steps)
         value = total_chains * steps / dt
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": eng.main_kernel, "kernel_ms": round(live_kern_ms, 5),
+                "kernel": kname, "kernel_ms": round(live_kern_ms, 5),
                 "kernel_ms_isolated": round(kern_ms, 5), "algorithmic_bytes_per_launch": int(alg_bytes)}
         if traffic_info:
             roof.update(traffic_info)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PSGLA_HIP_ABI_VERSION 4
+#define PSGLA_HIP_ABI_VERSION 5
 
 /* Max inner TV iterations the fused (temporally blocked) kernel handles. */
 #define PSGLA_TV_MAX_FUSED_IT 24
@@ -135,6 +135,14 @@ typedef struct PsglaTvStep {
                                  images run on the streaming kernel) needs the streaming kernel;
                                  the padding columns are scratch (never read into the image).
                                  The noise stream is indexed by the unpadded element.            */
+    int32_t multi_steps;      /* 0 / 1: one step per call.  > 1: ONE launch runs this many consecutive
+                                 steps (persistent tile kernel tv_tile_multi_kernel):
+                                 the tile kernel must be selected with every tile resident (grid <= CUs),
+                                 alpha == 1 (x2 NULL), launch_mask 0 / 3, norms_ring set, and arrive must
+                                 hold 4 ints ([1], [2] barrier / exit counters, [3] set to 1 if a barrier
+                                 wait timed out: the launch's results are then invalid)          */
+    double* norms_ring;       /* device [2][B][n_tv][2], zero-initialised: the multi-step kernel's
+                                 rel-err sums of steps s % 3 == 1, 2 (s % 3 == 0 uses norms)     */
 } PsglaTvStep;
 
 int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream);

@@ -100,6 +100,8 @@ struct TvArgs {
     int wave;                       // 1: per-wave pipeline kernel
     int wv_slots, wv_base, wv_extra, wv_whole;   // its row ranges (wave_item)
     unsigned long long* stamps;     // diagnostic build only (PSGLA_STAMPS): per-wave work/wait cycles
+    int msteps;                     // > 1: persistent multi-step tile kernel, this many steps per launch
+    double* norms_ring;             // its rel-err sums of steps s % 3 == 1, 2 ([2][B][n_tv][2]; s % 3 == 0: norms)
 };
 
 // Inner iterations (chunk-local) whose rel_err deepinv tests: global index >= 2 ("it > 1"); in the call's
@@ -1811,9 +1813,14 @@ struct TileShared {
     int s_flag, s_item, s_next;
 };
 
-template <bool EXACT, bool ALPHA1, int R>
+// RES (persistent multi-step kernel, section 3.1d of DESIGN.md): resident = the core rows' chain state
+// (x2 == X, u2) is still in the caller's registers from the previous step and the core rows' mean / sq in
+// sh.mst, so only the halo rows' X / u2 (the neighbour bands' outputs) and y / mask are loaded; the new
+// mean / sq rows are also written back to sh.mst.  nrm: the rel-err sums of this step.
+template <bool EXACT, bool ALPHA1, int R, bool RES = false>
 __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int plane, int band, int n_it,
-                                        bool track, long long step, bool fresh) {
+                                        bool track, long long step, bool fresh, float (&x2)[R][CPL],
+                                        float (&u0)[R][CPL], float (&u1)[R][CPL], bool resident, double* nrm) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int H = a.H, W = a.W, C = a.C, h = a.halo;
@@ -1832,10 +1839,12 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
     const bool need_prev = si.acc && !si.first;
     const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
-    float x2[R][CPL], u0[R][CPL], u1[R][CPL], z[R][CPL], yv[R][CPL];
+    float z[R][CPL], yv[R][CPL];
     int gi[R];
     bool rv[R], core[R];
     // ---- 1. every load of the tile in flight: state and observation to registers, mean / sq by DMA
+    // (RES: the state loads land straight in the state registers -- x2 == X for alpha == 1 --, and the
+    // rows whose state is resident load nothing; no second copy of the state is held)
     float4 fX[R], fY[R], fU0[R], fU1[R], fXS[R];
     uint32_t fM[R];
 #pragma unroll
@@ -1847,17 +1856,30 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
         fM[r] = 0u;
         if (rv[r] && colok) {
             const size_t base = poff + (size_t)gi[r] * W + gj0;
-            fX[r] = ld4(a.x[par_in] + base);
+            if (RES) {
+                if (!(resident && core[r])) {
+                    const float4 v = ld4(a.x[par_in] + base);
+                    x2[r][0] = v.x; x2[r][1] = v.y; x2[r][2] = v.z; x2[r][3] = v.w;
+                    if (!fresh) {
+                        const float4 p = ld4(a.u2[par_in] + 2 * base);
+                        const float4 q = ld4(a.u2[par_in] + 2 * base + 4);
+                        u0[r][0] = p.x; u1[r][0] = p.y; u0[r][1] = p.z; u1[r][1] = p.w;
+                        u0[r][2] = q.x; u1[r][2] = q.y; u0[r][3] = q.z; u1[r][3] = q.w;
+                    }
+                }
+            } else {
+                fX[r] = ld4(a.x[par_in] + base);
+                if (!fresh) {
+                    fU0[r] = ld4(a.u2[par_in] + 2 * base);
+                    fU1[r] = ld4(a.u2[par_in] + 2 * base + 4);
+                    if (!ALPHA1) fXS[r] = ld4(a.x2[par_in] + base);
+                }
+            }
             fY[r] = ld4(a.yobs + (size_t)b * a.y_cs + (size_t)c * HW + (size_t)gi[r] * W + gj0);
             fM[r] = *reinterpret_cast<const uint32_t*>(a.mask + (size_t)b * a.m_cs + (size_t)gi[r] * W + gj0);
-            if (!fresh) {
-                fU0[r] = ld4(a.u2[par_in] + 2 * base);
-                fU1[r] = ld4(a.u2[par_in] + 2 * base + 4);
-                if (!ALPHA1) fXS[r] = ld4(a.x2[par_in] + base);
-            }
         }
     }
-    if (need_prev && n_it >= 0) {
+    if (need_prev && n_it >= 0 && !(RES && resident)) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             if (rv[r] && core[r]) {
@@ -1878,13 +1900,16 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const bool ok = rv[r] && colok;
-        const float X[CPL] = {fX[r].x, fX[r].y, fX[r].z, fX[r].w};
+        const float X[CPL] = {RES ? x2[r][0] : fX[r].x, RES ? x2[r][1] : fX[r].y, RES ? x2[r][2] : fX[r].z,
+                              RES ? x2[r][3] : fX[r].w};
         const float yo[CPL] = {fY[r].x, fY[r].y, fY[r].z, fY[r].w};
         const float mk[CPL] = {(float)(fM[r] & 0xFFu), (float)((fM[r] >> 8) & 0xFFu), (float)((fM[r] >> 16) & 0xFFu),
                                (float)(fM[r] >> 24)};
         const float xs[CPL] = {fXS[r].x, fXS[r].y, fXS[r].z, fXS[r].w};
-        const float us0[CPL] = {fU0[r].x, fU0[r].z, fU1[r].x, fU1[r].z};
-        const float us1[CPL] = {fU0[r].y, fU0[r].w, fU1[r].y, fU1[r].w};
+        const float us0[CPL] = {RES ? u0[r][0] : fU0[r].x, RES ? u0[r][1] : fU0[r].z, RES ? u0[r][2] : fU1[r].x,
+                                RES ? u0[r][3] : fU1[r].z};
+        const float us1[CPL] = {RES ? u1[r][0] : fU0[r].y, RES ? u1[r][1] : fU0[r].w, RES ? u1[r][2] : fU1[r].y,
+                                RES ? u1[r][3] : fU1[r].w};
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
             float Y;
@@ -2023,8 +2048,8 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
             for (int ww = 0; ww < TV_NW; ++ww)
                 for (int q = 0; q < 4; ++q) { sd += sh.red[t][ww][q].x; sn += sh.red[t][ww][q].y; }
             if (!EXACT) sd *= (double)(a.rho * a.rho);     // fast sums hold (x - x2_prev)^2
-            atomicAdd(&a.norms[((size_t)b * a.n_tv + t) * 2], sd);
-            atomicAdd(&a.norms[((size_t)b * a.n_tv + t) * 2 + 1], sn);
+            atomicAdd(&nrm[((size_t)b * a.n_tv + t) * 2], sd);
+            atomicAdd(&nrm[((size_t)b * a.n_tv + t) * 2 + 1], sn);
         }
     }
     // ---- 6. the core rows out: X, u2 (x2), accumulators / block means, sample
@@ -2064,6 +2089,11 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
             }
             const float4 M4 = make_float4(m[0], m[1], m[2], m[3]);
             const float4 Q4 = make_float4(q[0], q[1], q[2], q[3]);
+            if (RES) {
+                // the next step's running mean / sq of this row (the wave's own LDS rows)
+                sh.mst[w * R + r][0][lane] = M4;
+                sh.mst[w * R + r][1][lane] = Q4;
+            }
             if (si.blockend) {
                 st_tile(a.blocks + (size_t)si.blk * BE + base, M4);
                 st_tile(a.blocks2 + (size_t)si.blk * BE + base, Q4);
@@ -2088,7 +2118,8 @@ __global__ void __launch_bounds__(TV_THREADS) tv_tile_kernel(const TvArgs a) {
         const int x = blockIdx.x, xcd = x & 7, k = x >> 3;
         const int plane = (k / T) * 8 + xcd;
         const int band = k - (k / T) * T;
-        if (plane < P) sb_tile<EXACT, ALPHA1, R>(a, sh, plane, band, a.n_tv, true, step, fresh);
+        float x2[R][CPL], u0[R][CPL], u1[R][CPL];
+        if (plane < P) sb_tile<EXACT, ALPHA1, R>(a, sh, plane, band, a.n_tv, true, step, fresh, x2, u0, u1, false, a.norms);
     }
 #ifdef PSGLA_ABL_TILE_NOFIN
     return;              // diagnostic timing build only: no arrival / finalisation
@@ -2154,7 +2185,8 @@ __global__ void __launch_bounds__(TV_THREADS) tv_tile_kernel(const TvArgs a) {
             const int plane = item / T, band = item - plane * T;
             const int nstop = __builtin_amdgcn_readfirstlane(sh.s_stop[plane / a.C]);
             if (nstop < a.n_tv) {
-                sb_tile<EXACT, ALPHA1, R>(a, sh, plane, band, nstop, false, step, fresh);
+                float x2[R][CPL], u0[R][CPL], u1[R][CPL];
+                sb_tile<EXACT, ALPHA1, R>(a, sh, plane, band, nstop, false, step, fresh, x2, u0, u1, false, a.norms);
                 wait_vm0();
                 __syncthreads();
             }
@@ -2166,6 +2198,154 @@ __global__ void __launch_bounds__(TV_THREADS) tv_tile_kernel(const TvArgs a) {
         *a.arrive = 0;
         if (a.fresh_dev) *a.fresh_dev = 0;
         if (a.advance_step && a.d_step) *a.d_step = step - a.step_offset + 1;   // the value read at the start: no dependent load
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Persistent multi-step tile kernel (alpha == 1, all tiles co-resident).
+//
+// One launch runs a.msteps consecutive Langevin steps of the tile kernel.  A tile's core rows keep
+// their chain state (X == x2, u2) in registers and their running mean / sq in LDS from one step to
+// the next, so a step loads only the halo rows' X / u2 (the neighbour bands' outputs of the previous
+// step) and y / mask; outputs are still stored every step (they are the halo of the neighbours and
+// the inputs of the rare early-stop redo).  Steps are separated by a grid barrier (every workgroup is
+// resident: the host launches this kernel only when grid <= CUs); after it EVERY workgroup reads all
+// chains' rel-err sums of the step and takes deepinv's early-stop decision itself, so no workgroup
+// waits for a last one to finalise.  A chain that stopped is recomputed by its own tiles from the
+// step's inputs (double-buffered, intact) and a second grid barrier publishes the redone rows.
+// The rel-err sums rotate over three buffers by step % 3: workgroup 0 clears the one of step s + 1
+// during step s (everyone finished reading it before arriving at barrier s - 1).  Barrier waits are
+// bounded (a.arrive[3] = 1 reports a timeout; the results of such a launch are invalid).
+// ---------------------------------------------------------------------------------------
+constexpr int GS_SPIN_MAX = 1 << 22;
+
+__device__ __forceinline__ double* step_norms(const TvArgs& a, long long step) {
+    const int m = (int)(((step % 3) + 3) % 3);
+    return m == 0 ? a.norms : a.norms_ring + (size_t)(m - 1) * a.B * a.n_tv * 2;
+}
+
+// Grid-wide barrier on counter gs[1] (monotonic within a launch): every wave has waited for its own
+// stores / atomics, then ONE wave per workgroup releases, waits (bounded) and acquires (the acquire
+// invalidates the CU's L1 and the XCD's L2 lines for the whole workgroup; an acquire by every wave
+// made the step 2.5x slower) before the workgroup barrier lets the other waves load.
+__device__ __forceinline__ void grid_sync(int* gs, int target) {
+    wait_vm0();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#ifndef PSGLA_MS_NOREL
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
+#ifdef PSGLA_MS_FLAG
+        // the last arriver publishes the barrier generation in gs[0]; the others poll that word (no
+        // polling loads on the line the arrival atomics serialise on)
+        const int old = __hip_atomic_fetch_add(&gs[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == target - 1) __hip_atomic_store(&gs[0], target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int* const pw = &gs[0];
+#else
+        __hip_atomic_fetch_add(&gs[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int* const pw = &gs[1];
+#endif
+        int spins = 0;
+        while (__hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > GS_SPIN_MAX) {
+                __hip_atomic_fetch_or(&gs[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+#ifdef PSGLA_MS_L1INV
+        asm volatile("buffer_inv sc0\n\ts_waitcnt vmcnt(0)" ::: "memory");
+#else
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+        wait_vm0();
+    }
+    __syncthreads();
+}
+
+template <bool EXACT, int R>
+__global__ void __launch_bounds__(TV_THREADS) tv_tile_multi_kernel(const TvArgs a) {
+    __shared__ TileShared<R> sh;
+    const long long step0 = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
+    const bool fresh0 = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
+    const int P = a.B * a.C;
+    const int T = a.nbands;
+    const int x = blockIdx.x, xcd = x & 7, k = x >> 3;
+    const int plane = (k / T) * 8 + xcd;            // all bands of a plane on one XCD (as tv_tile_kernel)
+    const int band = k - (k / T) * T;
+    const bool act = plane < P;
+    const int G = a.B;
+    const int NG = (int)gridDim.x;
+    const size_t nb = (size_t)a.B * a.n_tv * 2;
+    int* const gs = a.arrive;                       // [1] barrier count, [2] exit count, [3] timeout flag
+    float x2[R][CPL], u0[R][CPL], u1[R][CPL];       // the core rows' state, resident across steps
+    int target = 0;
+    for (int i = 0; i < a.msteps; ++i) {
+        const long long step = step0 + i;
+        const bool fresh = fresh0 && i == 0;
+        double* const nrm = step_norms(a, step);
+        if (act) sb_tile<EXACT, true, R, true>(a, sh, plane, band, a.n_tv, true, step, fresh, x2, u0, u1, i > 0, nrm);
+        if (blockIdx.x == 0) {
+            double* const nx = step_norms(a, step + 1);
+            for (size_t j = threadIdx.x; j < nb; j += blockDim.x)
+                __hip_atomic_store(&nx[j], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        target += NG;
+        grid_sync(gs, target);
+#ifdef PSGLA_MS_NODECIDE
+        continue;            // diagnostic timing build only: no early-stop decision
+#endif
+        // deepinv's early stop of every chain, decided by every workgroup from the step's sums
+        for (int g = threadIdx.x; g < G; g += blockDim.x) sh.s_stop[g] = 0;
+        if (threadIdx.x == 0) sh.s_item = 0;
+        __syncthreads();
+        for (int j = threadIdx.x; j < G * MAXIT; j += blockDim.x) {
+            const int g = j / MAXIT, t = j - g * MAXIT;
+            if (t >= trk_lo(a) && t <= trk_hi(a) && t < a.n_tv) {
+                const double nd = __hip_atomic_load(&nrm[((size_t)g * a.n_tv + t) * 2], __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+                const double nn = __hip_atomic_load(&nrm[((size_t)g * a.n_tv + t) * 2 + 1], __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+                const float rel = (float)sqrt(nd) / (float)sqrt(nn);
+                if (rel < a.tol) atomicOr(&sh.s_stop[g], 1 << t);
+            }
+        }
+        __syncthreads();
+        for (int g = threadIdx.x; g < G; g += blockDim.x) {
+            const int m = sh.s_stop[g];
+            sh.s_stop[g] = m ? (__ffs(m) - 1) + 1 : a.n_tv;
+            if (m) sh.s_item = 1;
+        }
+        __syncthreads();
+        if (sh.s_item) {
+            // rare: the tiles of a stopped chain are recomputed from the step's inputs with the stopped count
+            const int nstop = act ? sh.s_stop[plane / a.C] : a.n_tv;
+            if (act && nstop < a.n_tv)
+                sb_tile<EXACT, true, R, true>(a, sh, plane, band, nstop, false, step, fresh, x2, u0, u1, false, nrm);
+            target += NG;
+            grid_sync(gs, target);
+        }
+    }
+    // ---- exit: the last workgroup out clears the counters and every rel-err buffer, advances the step
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int old = __hip_atomic_fetch_add(&gs[2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sh.s_flag = (old == NG - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!sh.s_flag) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    for (size_t j = threadIdx.x; j < nb; j += blockDim.x) {
+        a.norms[j] = 0.0;
+        a.norms_ring[j] = 0.0;
+        a.norms_ring[nb + j] = 0.0;
+    }
+    if (threadIdx.x == 0) {
+        gs[0] = 0;
+        gs[1] = 0;
+        gs[2] = 0;
+        if (a.fresh_dev) *a.fresh_dev = 0;
+        if (a.advance_step && a.d_step) *a.d_step = step0 - a.step_offset + a.msteps;
     }
 }
 
@@ -3899,6 +4079,12 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
             hipLaunchKernelGGL((tv_wave_kernel<EXACT, ALPHA1>), dim3(s.wv_slots / WV_NW), dim3(WV_THREADS), 0, st, s);
             return launch_check("tv_wave_kernel");
         }
+        if (FRONT == FRONT_INPAINT && a.tile_r > 0 && a.msteps > 1) {
+            if (!ALPHA1 || a.tile_r != 3 || mask != 3) return fail(0, "psgla_tv_step: multi_steps needs alpha == 1 and a full launch");
+            const int grid = ((P + 7) / 8) * 8 * a.nbands;
+            hipLaunchKernelGGL((tv_tile_multi_kernel<EXACT, 3>), dim3(grid), dim3(TV_THREADS), 0, st, a);
+            return launch_check("tv_tile_multi_kernel");
+        }
         if (FRONT == FRONT_INPAINT && a.tile_r > 0) {
             TvArgs s = a;
             s.fin_inline = (mask & 2) ? 1 : 0;
@@ -4050,6 +4236,15 @@ int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream) {
     a.samples = s->samples; a.samples_cap = s->samples_cap;
     a.blocks = s->blocks; a.blocks2 = s->blocks2; a.blocks_cap = s->blocks_cap;
     if (select_step_kernel(d, a) < 0) return g_sel_err == g_err ? (int)hipErrorInvalidValue : fail(0, g_sel_err);
+    if (d->multi_steps > 1) {
+        // persistent multi-step tile kernel: every tile co-resident (grid barrier), alpha == 1
+        if (a.tile_r != 3 || !alpha1 || !d->norms_ring || (d->launch_mask != 0 && d->launch_mask != 3))
+            return fail(0, "psgla_tv_step: multi_steps > 1 needs the tile kernel, alpha == 1, norms_ring and a full launch");
+        const long long grid = ((long long)(d->B * d->C + 7) / 8) * 8 * a.nbands;
+        if (grid > device_cus()) return fail(0, "psgla_tv_step: multi_steps > 1 needs every tile resident (grid > CUs)");
+        a.msteps = d->multi_steps;
+        a.norms_ring = d->norms_ring;
+    }
     hipStream_t st = (hipStream_t)stream;
     const int m = d->launch_mask;
     if (d->exact)

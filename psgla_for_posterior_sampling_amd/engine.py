@@ -25,7 +25,7 @@ class FusedTvChains:
                  n_inter: int, n_inter_mmse: int, chain0: int = 0, exact: bool = False,
                  tv_x2: torch.Tensor | None = None, tv_u2: torch.Tensor | None = None,
                  store_samples: bool = True, store_blocks: bool = True, kernel_variant: str = "auto",
-                 stream_wgs: int = 0):
+                 stream_wgs: int = 0, multi_step: bool = False):
         if init.dim() != 4:
             raise ValueError("init must be (B, C, H, W)")
         if tv.n_it > N.TV_MAX_FUSED_IT:
@@ -88,9 +88,11 @@ class FusedTvChains:
         d.fresh = self.work.fresh.data_ptr()
         d.norms = self.work.norms.data_ptr()
         d.arrive = self.work.arrive.data_ptr()
+        d.norms_ring = self.work.norms_ring.data_ptr()
         d.kernel_variant = {"auto": 0, "band": 1, "stream": 2, "p2p": 3, "tile": 4, "wave": 5}[kernel_variant]
         d.stream_wgs = int(stream_wgs)
         self.desc = d
+        self.multi_step = bool(multi_step)
         self.sched_struct = self.sched.struct(True, 0)
         if self.warm_first:
             # first step of a warm-started run: the TV primal x2 (previous run's state) is not X
@@ -131,16 +133,33 @@ class FusedTvChains:
                 self._launch(self.desc)
             self.steps_done += 1
 
+    @property
+    def multi_step_active(self) -> bool:
+        """Graph segments run as ONE persistent multi-step launch (tv_tile_multi_kernel):
+        opt-in (multi_step=True; measured slower than one tile-kernel launch per step), when the tile kernel
+        is selected with every tile resident and alpha == 1."""
+        if not (self.multi_step and self.alpha1) or self.main_kernel != "tv_tile_kernel":
+            return False
+        B, C, H, _ = self.shape
+        bands = -(-H // (48 - 2 * self.desc.n_tv)) if H > 48 else 1
+        return -(-(B * C) // 8) * 8 * bands <= torch.cuda.get_device_properties(self.device).multi_processor_count
+
     def capture(self, steps_per_graph: int):
-        """Capture `steps_per_graph` identical steps into one hipGraph (after step 0)."""
+        """Capture `steps_per_graph` identical steps into one hipGraph (after step 0): one launch per
+        step, or one persistent launch for all of them (multi_step_active)."""
         if self.steps_done == 0 and self.warm_first:
             self.step(1)
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=s):
-            for _ in range(steps_per_graph):
-                self._launch(self.desc)
+            if steps_per_graph > 1 and self.multi_step_active:
+                dm = N.PsglaTvStep.from_buffer_copy(self.desc)
+                dm.multi_steps = steps_per_graph
+                self._launch(dm)
+            else:
+                for _ in range(steps_per_graph):
+                    self._launch(self.desc)
         torch.cuda.current_stream().wait_stream(s)
         self.graph = g
         self.graph_steps = steps_per_graph

@@ -813,6 +813,42 @@ def test_tile_kernel_early_stop_handoff_full_size(tol):
     assert not torch.equal(outs[("tile", tol)][3], outs[("tile", 1e-5)][3]), "no early stop fired"
 
 
+@pytest.mark.parametrize("exact,tol", [(False, 1e-5), (True, 1e-5), (False, 3e-3), (True, 1e-3)])
+def test_tile_multi_step_equals_per_step_full_size(exact, tol):
+    """The persistent multi-step tile kernel (one launch per 10-step graph segment, core-row state resident
+    in registers / LDS across steps, grid barrier between steps, every workgroup deciding deepinv's early
+    stop) against one tile-kernel launch per step: 8 chains at 3 x 256 x 256, 40 steps, samples, block
+    means, final X and u2 bit-identical, with and without firing early stops; no barrier wait timed out."""
+    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    B = 8
+    g = torch.Generator(device=DEV).manual_seed(31)
+    xs = torch.rand((B, 3, 256, 256), generator=g, device=DEV)
+    gen = torch.Generator(device=DEV).manual_seed(0)
+    mask2d = (torch.rand((256, 256), generator=gen, device=DEV) > 0.5).to(torch.uint8)
+    y = mask2d.float() * xs + torch.normal(torch.zeros_like(xs), std=(1 / 255.0) * torch.ones_like(xs),
+                                           generator=gen)
+    init = (mask2d.float() * y + (1 - mask2d.float()) * 0.5).contiguous()
+    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
+    outs = []
+    for multi in (True, False):
+        eng = FusedTvChains(init, y.contiguous(), mask2d, c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
+                            alpha=1.0, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10, tol=tol),
+                            seed=0, n_iter=41, n_inter=10, n_inter_mmse=10, exact=exact, multi_step=multi)
+        assert eng.multi_step_active == multi
+        eng.step(1)                       # eager first step (fresh TV start), then 4 graph segments
+        eng.capture(10)
+        eng.replay(4)
+        torch.cuda.synchronize()
+        assert int(eng.work.arrive[3].item()) == 0, "grid barrier wait timed out"
+        assert int(eng.sched.d_step.item()) == 41
+        assert float(eng.work.norms.abs().sum()) == 0.0 and float(eng.work.norms_ring.abs().sum()) == 0.0
+        bm, bm2 = eng.blocks()
+        outs.append((eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("B,H,W,alpha,tol,n_tv", [
     (3, 48, 64, 1.0, 1e-5, 10),      # 3 ranges per plane: halo cuts at both ends
     (2, 100, 64, 1.0, 1e-5, 10),     # 6 ranges per plane
