@@ -19,11 +19,12 @@ y = m * x + torch.normal(torch.zeros_like(x), std=1 / 255.0, generator=g)
 init = m * y + (~m) * 0.5
 s = 10 / 255.0
 h = hashlib.sha256()
-for wgs in (0, -1):
+for wgs, variant, exact in ((0, "auto", False), (-1, "stream", False), (0, "stream", False), (0, "tile", True),
+                           (0, "stream", True)):
     eng = FusedTvChains(init.contiguous(), y.contiguous(), m.to(torch.uint8), c1=float(s * s / 10.0),
                         c2=float(2 ** 0.5 * s), sigma2=(1 / 255.0) ** 2, alpha=1.0, ths=s,
                         tv=K.TvConstants(n_it_max=10), seed=1, n_iter=40, n_inter=10, n_inter_mmse=10,
-                        exact=False, stream_wgs=wgs)
+                        exact=exact, stream_wgs=wgs, kernel_variant=variant)
     eng.run(40, graph_steps=0)
     torch.cuda.synchronize()
     bm, bm2 = eng.blocks()
