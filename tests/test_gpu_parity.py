@@ -831,9 +831,10 @@ def test_tile_multi_step_equals_per_step_full_size(exact, tol):
     init = (mask2d.float() * y + (1 - mask2d.float()) * 0.5).contiguous()
     c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
     outs = []
-    for multi in (True, False):
+    runs = [(True, tol), (False, tol)] + ([(True, 1e-5)] if tol > 1e-5 else [])
+    for multi, t in runs:
         eng = FusedTvChains(init, y.contiguous(), mask2d, c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
-                            alpha=1.0, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10, tol=tol),
+                            alpha=1.0, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10, tol=t),
                             seed=0, n_iter=41, n_inter=10, n_inter_mmse=10, exact=exact, multi_step=multi)
         assert eng.multi_step_active == multi
         eng.step(1)                       # eager first step (fresh TV start), then 4 graph segments
@@ -845,8 +846,10 @@ def test_tile_multi_step_equals_per_step_full_size(exact, tol):
         assert float(eng.work.norms.abs().sum()) == 0.0 and float(eng.work.norms_ring.abs().sum()) == 0.0
         bm, bm2 = eng.blocks()
         outs.append((eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone()))
-    for a, b in zip(*outs):
+    for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
+    if len(outs) > 2:
+        assert not torch.equal(outs[0][3], outs[2][3]), "no early stop fired"
 
 
 @pytest.mark.parametrize("B,H,W,alpha,tol,n_tv", [
