@@ -24,12 +24,12 @@ block slots), barrier + synchronize on both sides, max over ranks.  value = chai
 
 Warm-up: the W steps (eager + graph capture), then untimed graph replays until at least
 --warmup-seconds of GPU work have run (clocks and power state settle; reported as
-`warmup_s`), after which the step index is rewound to where the timed steps of a W-step
-warm-up would start -- the timed steps write the same sample / block slots as in a run that
-warmed up for W steps (the chain state simply continues).
+`warmup_s`), after which the chain state, accumulators, TV state and step index are restored
+from a snapshot taken before them: the timed steps are exactly those of a run that warmed up
+for W steps, on every rank, whatever the wall-clock warm-up ran.
 
 The roofline figure divides the algorithmic bytes of one launch by the dominant kernel's
-(tv_stream_kernel: one launch per step) average duration from HIP events recorded on the
+(tv_pair_kernel at 64 chains per GPU: one launch per step) average duration from HIP events recorded on the
 replay stream around the timed region; the kernel re-launched alone on its own stream is
 reported beside it (kernel_ms_isolated) as a cross-check.  `traffic` (HBM bytes per launch
 from rocprofv3 PMC counters) cannot be collected inside an un-profiled run: it is read from
@@ -53,6 +53,7 @@ METRIC = "Langevin steps/sec (3×256×256, batch=64) at 1/2/4/8 GPU; HBM GB/s vs
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # committed PMC summaries (tools/profile_round.sh + tools/pmc_summary.py) by dominant kernel
 PMC_PROFILES = {"tv_stream_kernel": os.path.join("profiles", "r02e_pmc_tv_stream.json"),
+                "tv_pair_kernel": os.path.join("profiles", "r03_pmc_tv_pair.json"),
                 "tv_tile_kernel": os.path.join("profiles", "r02e_pmc_tv_tile.json")}
 
 
@@ -72,12 +73,11 @@ def parse():
     p.add_argument("--kernel-iters", type=int, default=50)
     p.add_argument("--tv-iters", type=int, default=10, help="TV n_it_max (analysis only; the workload is 10)")
     p.add_argument("--stream-wgs", type=int, default=0, help="stream kernel work split (0 auto, -1 per plane)")
-    p.add_argument("--variant", choices=["auto", "band", "stream", "p2p", "tile", "wave"], default="auto", help="fused TV kernel (analysis)")
+    p.add_argument("--variant", choices=["auto", "band", "stream", "pair", "tile"], default="auto",
+                   help="fused TV kernel (analysis; auto = the library's choice)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the batch-1 CPU leg")
     p.add_argument("--cpu-b64-steps", type=int, default=10, help="timed steps of the batch-64 CPU leg (0: skip)")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--multi-step", action="store_true",
-                   help="graph segments as one persistent multi-step tile-kernel launch (analysis; DESIGN.md 3.1d)")
     p.add_argument("--pmc-json", default=None, help="PMC summary to report as roofline.traffic (default: the "
                    "committed profile of the dispatched kernel, when it was measured on this workload)")
     return p.parse_args()
@@ -117,7 +117,20 @@ def cpu_baseline(seconds: float, b64_steps: int):
     tests/golden), at batch 1 (as the reference runs, bounded by `seconds`) and at batch 64
     (the benched workload; `b64_steps` steps, one psgla call -- the reference needs n_iter >= 10)."""
     from oracle import psgla_oracle as orc
+    # threads: torch's intra-op pool, i.e. OMP_NUM_THREADS where the harness sets it (the GPU box gives one
+    # GPU's job a 16-CPU share of the host; os.cpu_count() there counts the whole machine).  Reported
+    # beside the affinity-allowed and logical CPU counts and the cgroup CPU quota.
     threads = torch.get_num_threads()
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
     s = 10 / 255.0
     alpha = torch.tensor(1.0)
     lam = torch.tensor(10.0)
@@ -148,7 +161,8 @@ def cpu_baseline(seconds: float, b64_steps: int):
     out = {"value": round(b1, 2), "unit": "image-steps/s", "cores": threads, "kind": "port",
            "sample": f"batch 1: {steps} PSGLA+TV steps (3x256x256) after 10 warm-up steps, {dt1:.1f} s",
            "batch1_image_steps_per_s": round(b1, 2), "cpu_model": cpu_model(), "threads": threads,
-           "host_logical_cpus": os.cpu_count()}
+           "host_logical_cpus": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+           "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
     if b64_steps > 0:
         dg, X = problem(64)
         tv = orc.TVDenoiser(n_it_max=10)
@@ -223,15 +237,17 @@ def main():
                         sigma2=float(np.float32(sigma1 ** 2)), alpha=1.0, ths=float(np.float32(s)),
                         tv=K.TvConstants(n_it_max=args.tv_iters), seed=0, n_iter=n_iter + args.kernel_iters,
                         n_inter=n_inter, n_inter_mmse=nm, chain0=c0, exact=args.exact,
-                        stream_wgs=args.stream_wgs, kernel_variant=args.variant,
-                        multi_step=args.multi_step)
+                        stream_wgs=args.stream_wgs, kernel_variant=args.variant)
     # warm-up: eager steps + graph capture + one replay
     eng.step(w_eager)
     eng.capture(gs)
     eng.replay(1)
     torch.cuda.synchronize()
     step0 = eng.steps_done
-    # time-based warm-up: replays until >= warmup_seconds of GPU work, then rewind the step index
+    # time-based warm-up: replays until >= warmup_seconds of GPU work, then the chain state, accumulators
+    # and step index are restored to where they were, so the timed steps (and the reported PSNR) are
+    # those of a run that warmed up for exactly W steps, whatever the wall-clock warm-up ran
+    snap = eng.snapshot()
     tw0 = time.perf_counter()
     n_warm = 0
     while time.perf_counter() - tw0 < args.warmup_seconds:
@@ -241,6 +257,9 @@ def main():
             n_warm += gs
         torch.cuda.synchronize()
     warmup_s = time.perf_counter() - tw0
+    eng.restore(snap)
+    del snap
+    torch.cuda.synchronize()
 
     def barrier():
         if world > 1:
@@ -289,9 +308,7 @@ def main():
     psnr_sum, n_chains = reduce_psnr(blocks, xs, world)
 
     traffic, traffic_info = None, None
-    # the kernel the timed graphs launch: one persistent launch per graph segment when the tile kernel's
-    # tiles are all resident (tv_tile_multi_kernel), else one launch of main_kernel per step
-    kname = "tv_tile_multi_kernel" if (gs > 1 and eng.multi_step_active) else eng.main_kernel
+    kname = eng.main_kernel            # the kernel the timed graphs launch, once per step
     pmc_json = args.pmc_json or os.path.join(REPO, PMC_PROFILES.get(kname, "none"))
     if os.path.exists(pmc_json):
         try:

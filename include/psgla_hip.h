@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PSGLA_HIP_ABI_VERSION 5
+#define PSGLA_HIP_ABI_VERSION 6
 
 /* Max inner TV iterations the fused (temporally blocked) kernel handles. */
 #define PSGLA_TV_MAX_FUSED_IT 24
@@ -72,20 +72,19 @@ typedef struct PsglaSchedule {
  * k >= 2, per chain: the affected chains are recomputed with k+1 inner iterations)
  * is honoured, `fresh` is cleared and *d_step advanced once the step is complete.
  * What is launched depends on the variant the shape selects (kernel_variant 0):
- *   - the row-streaming kernel (tv_stream_kernel: row pitch ldw % 4 == 0, 1 <= n_tv <= 10,
- *     H >= 2, every width with column segments): ONE launch per step; its last
- *     workgroup to finish evaluates the early stop, re-streams stopped chains and
- *     advances the step (no second kernel);
  *   - the small-batch tile kernel (tv_tile_kernel: W <= 256, W % 4 == 0) when its
- *     48-row tiles all fit on the CUs at once (few chains per GPU): ONE launch,
- *     finalised by its last workgroup like the stream kernel;
+ *     48-row tiles all fit on the CUs at once (few chains per GPU): ONE launch; its last
+ *     workgroup to finish evaluates the early stop, recomputes stopped chains and advances
+ *     the step (no second kernel);
+ *   - else the row-pair pipeline (tv_pair_kernel: W <= 256, W % 4 == 0, ldw == W,
+ *     alpha == 1 i.e. x2 == NULL, 1 <= n_tv <= 10, H >= 2): two rows per pipeline step,
+ *     ONE launch, finalised in-kernel the same way;
+ *   - else the row-streaming kernel (tv_stream_kernel: row pitch ldw % 4 == 0,
+ *     1 <= n_tv <= 10, H >= 2, every width with column segments, any alpha): one row per
+ *     pipeline step, ONE launch, finalised in-kernel;
  *   - otherwise (n_tv > 10 or H < 2, or kernel_variant 1) the temporally blocked
  *     band kernel (tv_main_kernel) followed by a small finaliser kernel
- *     (tv_finalise_kernel, <= 8 workgroups) that does the same;
- *   - only when forced (kernel_variant 5; W <= 256, W % 4 == 0, ldw == W, 1 <= n_tv <= 10,
- *     H >= 2) the per-wave pipeline kernel (tv_wave_kernel: each wave runs front, all inner
- *     iterations and back of its own row range of one plane, state in registers; ONE launch,
- *     finalised by its last workgroup; slower than the stream kernel at 64 chains).
+ *     (tv_finalise_kernel, <= 8 workgroups) that does the same.
  * launch_mask 1 launches only the main pass of either variant (timing).
  * ------------------------------------------------------------------------------- */
 typedef struct PsglaTvStep {
@@ -114,18 +113,10 @@ typedef struct PsglaTvStep {
     int32_t* arrive;          /* device int, zero-initialised (finaliser arrival counter)   */
     int32_t launch_mask;      /* 0 or 3: both kernels; 1: tile kernel only (re-runs the same step:
                                  idempotent, for kernel timing); 2: finaliser only            */
-    int32_t kernel_variant;   /* 0: auto (row-streaming pipeline when W % 4 == 0 and n_tv <= 10,
-                                 else temporally blocked bands); 1: force bands; 2: force stream
-                                 (one workgroup barrier per pipeline step); 3: force stream with
-                                 point-to-point LDS progress waits instead of the barrier; 4: force
-                                 the small-batch tile kernel (W <= 256, W % 4 == 0, ldw == W); 5: force
-                                 the per-wave pipeline kernel (same shape limits, 1 <= n_tv <= 10).  Auto
-                                 picks the tile kernel when its tiles (one per workgroup, 48 rows
-                                 incl. n_tv halo rows) all fit on the CUs at once, else the stream */
-    uint64_t* debug_stamps;   /* diagnostic builds only (-DPSGLA_STAMPS), else NULL: [workgroups][16][2]
-                                 work / wait shader cycles per wave of the streaming kernel, then
-                                 [steps][16][2] barrier arrival / release times of workgroup 0,
-                                 then [workgroups][4][4] front-wave segment cycles (tools/stamps.py) */
+    int32_t kernel_variant;   /* 0: auto (see above); 1: force the band kernel; 2: force the row stream
+                                 (one row per pipeline step); 3: force the row-pair pipeline (W <= 256,
+                                 W % 4 == 0, ldw == W, alpha == 1); 4: force the small-batch tile kernel
+                                 (W <= 256, W % 4 == 0, ldw == W).  Other values are rejected. */
     int32_t stream_wgs;       /* streaming kernel work split: 0 auto (rows of all planes cut into
                                  one contiguous range per CU, n_tv halo rows at cuts, when W <= 256);
                                  -1 one workgroup per plane; > 0 force that many row ranges      */
@@ -135,21 +126,12 @@ typedef struct PsglaTvStep {
                                  images run on the streaming kernel) needs the streaming kernel;
                                  the padding columns are scratch (never read into the image).
                                  The noise stream is indexed by the unpadded element.            */
-    int32_t multi_steps;      /* 0 / 1: one step per call.  > 1: ONE launch runs this many consecutive
-                                 steps (persistent tile kernel tv_tile_multi_kernel):
-                                 the tile kernel must be selected with every tile resident (grid <= CUs),
-                                 alpha == 1 (x2 NULL), launch_mask 0 / 3, norms_ring set, and arrive must
-                                 hold 4 ints ([1], [2] barrier / exit counters, [3] set to 1 if a barrier
-                                 wait timed out: the launch's results are then invalid)          */
-    double* norms_ring;       /* device [2][B][n_tv][2], zero-initialised: the multi-step kernel's
-                                 rel-err sums of steps s % 3 == 1, 2 (s % 3 == 0 uses norms)     */
 } PsglaTvStep;
 
 int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream);
 /* Which kernel psgla_tv_step launches for this descriptor (host-side query, launches nothing):
- * 0 band kernel + finaliser, 1 row stream, 2 row stream with P2P waits, 3 small-batch tile kernel
- * (one launch, finalised by its last workgroup), 4 per-wave pipeline kernel (one launch, finalised by
- * its last workgroup); -1 if the descriptor is rejected. */
+ * 0 band kernel + finaliser, 1 row stream (tv_stream_kernel), 2 row-pair pipeline (tv_pair_kernel),
+ * 3 small-batch tile kernel (tv_tile_kernel); -1 if the descriptor is rejected. */
 int psgla_tv_step_kernel(const PsglaTvStep* d);
 
 /* ---------------------------------------------------------------------------------

@@ -29,6 +29,7 @@
 #include <cfloat>
 #include <cmath>
 #include <stdint.h>
+#include <type_traits>
 #include <stdio.h>
 #include <string.h>
 
@@ -95,13 +96,8 @@ struct TvArgs {
     int split_wgs;                  // stream kernel: > 0 = row-split mode over this many workgroups
     int st_nsegs, st_seg_w, st_halo;  // stream kernel column segmentation (W > 256)
     int fin_inline;                 // stream kernel: 1 = the last workgroup finalises the step
-    int p2p;                        // stream kernel: 1 = point-to-point LDS progress waits instead of barriers
     int tile_r;                     // > 0: small-batch tile kernel with tile_r rows per wave (one tile per workgroup)
-    int wave;                       // 1: per-wave pipeline kernel
-    int wv_slots, wv_base, wv_extra, wv_whole;   // its row ranges (wave_item)
-    unsigned long long* stamps;     // diagnostic build only (PSGLA_STAMPS): per-wave work/wait cycles
-    int msteps;                     // > 1: persistent multi-step tile kernel, this many steps per launch
-    double* norms_ring;             // its rel-err sums of steps s % 3 == 1, 2 ([2][B][n_tv][2]; s % 3 == 0: norms)
+    int pair;                       // stream kernel: 1 = the row-pair pipeline (tv_pair_kernel)
 };
 
 // Inner iterations (chunk-local) whose rel_err deepinv tests: global index >= 2 ("it > 1"); in the call's
@@ -121,18 +117,6 @@ __device__ __forceinline__ float f4get(const float4& v, int k) {
 // quad_perm, then row rotations by 4 and 8: every lane holds its row's sum), then the four row sums
 // read out by v_readlane: pure VALU, no LDS round trips (a __shfl_xor tree is six dependent
 // ds_bpermute's, ~0.5 us per tracked TV iteration on the tile kernel's critical path).
-#ifdef PSGLA_WAVESUM_SHFL
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-__device__ __forceinline__ float2 row_sum2(float a, float b) {
-#pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) { a += __shfl_xor(a, o); b += __shfl_xor(b, o); }
-    return make_float2(a, b);
-}
-#else
 #define PSGLA_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), (ctrl), 0xF, 0xF, false))
 __device__ __forceinline__ float wave_sum(float v) {
     v += PSGLA_DPP(v, 0xB1);      // quad_perm [1,0,3,2]: lane ^ 1
@@ -154,7 +138,6 @@ __device__ __forceinline__ float2 row_sum2(float a, float b) {
     return make_float2(a, b);
 }
 #undef PSGLA_DPP
-#endif
 
 // Block-mean accumulator + sample storage for one element (restoration_algorithms.py:240-271).
 // idx = chain*E + e within the batch; BE = B*E (slot stride of samples/blocks).
@@ -521,9 +504,6 @@ __global__ void __launch_bounds__(TV_THREADS) tv_finalise_kernel(const TvArgs a)
     const int P = a.B * a.C;
     const int T = a.tiles;
     const int G = a.per_chain_norm ? a.B : 1;
-#ifdef FIN_EMPTY
-    if (a.B > 0) return;
-#endif
     if (threadIdx.x == 0) s_flag = 0;
     __syncthreads();
     for (int g = threadIdx.x; g < G; g += blockDim.x) {
@@ -560,9 +540,7 @@ __global__ void __launch_bounds__(TV_THREADS) tv_finalise_kernel(const TvArgs a)
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-#ifndef FIN_NOFENCE
         __threadfence();
-#endif
         const int old = atomicAdd(a.arrive, 1);
         s_flag = (old == (int)gridDim.x - 1) ? 2 : 0;
     }
@@ -617,10 +595,6 @@ struct StreamShared {
     uint32_t fmk[SP_FRONT][2][WAVE];
     float4 bst[SP_BACK][2][2][WAVE];
     float red[SP_MAXSEG][SP_MAXST][2];
-    // P2P pipelines: prog[w] = steps of the pass whose shared-LDS work wave w has completed (its ring /
-    // Y-ring reads landed and writes performed); p2p_fail: a progress wait ran out (bounded spin)
-    uint32_t prog[16];
-    uint32_t p2p_fail;
 };
 
 typedef __attribute__((address_space(1))) const void* gptr_t;
@@ -631,55 +605,15 @@ typedef float v4f_t __attribute__((ext_vector_type(4)));
 // Issued as inline asm: the compiler does not track these loads, so it cannot insert a
 // conservative vmcnt(0) before unrelated LDS accesses -- the waves wait with counted
 // s_waitcnt vmcnt(N) themselves (vector-memory operations retire in issue order).
-// PSGLA_DMA_AUX: cache-policy bits of the LDS-DMA loads (diagnostic A/B builds; default none)
-#if defined(PSGLA_DMA_POL) && PSGLA_DMA_POL == 1
-#define PSGLA_DMA_AUX " nt"
-#elif defined(PSGLA_DMA_POL) && PSGLA_DMA_POL == 2
-#define PSGLA_DMA_AUX " sc1"
-#elif defined(PSGLA_DMA_POL) && PSGLA_DMA_POL == 3
-#define PSGLA_DMA_AUX " sc0 sc1 nt"
-#else
-#define PSGLA_DMA_AUX ""
-#endif
 __device__ __forceinline__ void glds16(const void* src, void* dst) {
     const unsigned off = (unsigned)(size_t)(lptr_t)dst;
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" PSGLA_DMA_AUX
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
                  :: "v"(src), "s"(off) : "memory", "m0");
 }
 __device__ __forceinline__ void glds4(const void* src, void* dst) {
     const unsigned off = (unsigned)(size_t)(lptr_t)dst;
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" PSGLA_DMA_AUX
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off"
                  :: "v"(src), "s"(off) : "memory", "m0");
-}
-// SGPR-base forms (per-wave pipeline kernel): global_* with a wave-uniform 64-bit base in SGPRs (saddr) and
-// a 32-bit per-lane byte offset in one VGPR -- no 64-bit per-lane address stays live across the row loop
-// (a spilled one is reloaded behind a compiler vmcnt(0) that serialises the hand-placed DMAs).  No
-// immediate offsets (an LDS-DMA's would also move its LDS destination).
-// The base is wave-uniform by construction at every call site; readfirstlane makes that provable where
-// the compiler cannot see it (free when the value already sits in SGPRs).  The asm opens with s_nop 4:
-// a VMEM instruction reading an SGPR that a VALU (v_readfirstlane) wrote needs 5 wait states, and the
-// compiler does not pad hazards into inline asm (without it the loads read a stale base: memory fault).
-__device__ __forceinline__ const void* uni_ptr(const void* p) {
-    const uint64_t v = (uint64_t)p;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return (const void*)(((uint64_t)hi << 32) | lo);
-}
-// 16 B (4 B) per lane straight into LDS: lane i lands at dst + 16 i (4 i)
-__device__ __forceinline__ void sglds16(const void* sbase, uint32_t voff, void* dst) {
-    const unsigned m = (unsigned)(size_t)(lptr_t)dst;
-    asm volatile("s_nop 4\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
-                 :: "v"(voff), "s"(uni_ptr(sbase)), "s"(m) : "memory", "m0");
-}
-__device__ __forceinline__ void sglds4(const void* sbase, uint32_t voff, void* dst) {
-    const unsigned m = (unsigned)(size_t)(lptr_t)dst;
-    asm volatile("s_nop 4\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1"
-                 :: "v"(voff), "s"(uni_ptr(sbase)), "s"(m) : "memory", "m0");
-}
-// 16-B streaming (nt) store; s_nop: the store-data hazard the compiler cannot see
-__device__ __forceinline__ void sgst16(void* sbase, uint32_t voff, const float4& v) {
-    const v4f_t x = {v.x, v.y, v.z, v.w};
-    asm volatile("s_nop 4\n\tglobal_store_dwordx4 %0, %1, %2 nt\n\ts_nop 1" :: "v"(voff), "v"(x), "s"(uni_ptr(sbase)) : "memory");
 }
 // Workgroup barrier that only drains LDS (lgkmcnt): LDS-DMA loads stay in flight across it
 // (a __syncthreads() fence would wait vmcnt(0) while a global_load_lds is pending).
@@ -705,9 +639,6 @@ __device__ __forceinline__ void wait_vm_n(int n) { wait_vm_le<0>(n); }
 // release before the arrival count still writes back whatever the XCD's L2 holds dirty).
 typedef float v4f __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st_nt(float* p, const float4& v) {
-#ifdef PSGLA_ABL_NOSTORE
-    if (p) return;      // diagnostic timing build only: outputs are not written
-#endif
     const v4f x = {v.x, v.y, v.z, v.w};
     // s_nop: the compiler does not see this store, so it cannot pad the store-data hazard
     // (a VALU write of the data VGPRs right after a >8-byte store) -- the asm does
@@ -718,139 +649,12 @@ __device__ __forceinline__ void st_nt(float* p, const float4& v) {
 // and each then releases (writes back) its XCD's dirty L2 lines before the arrival count, which
 // write-through stores leave clean; -DPSGLA_TILE_ST_NT: nt stores as the stream kernel.
 __device__ __forceinline__ void st_tile(float* p, const float4& v) {
-#ifdef PSGLA_ABL_NOSTORE
-    if (p) return;      // diagnostic timing build only: outputs are not written
-#endif
-#if defined(PSGLA_TILE_ST_NT)
-    st_nt(p, v);
-#else
     const v4f x = {v.x, v.y, v.z, v.w};
     asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
-#endif
 }
 
-// Diagnostic build (-DPSGLA_STAMPS): every wave accumulates the cycles it spends working
-// between two pipeline barriers and the cycles it waits at them (s_memtime, shader clock).
-struct Stamps {
-    unsigned long long work = 0, wait = 0, t0 = 0;
-    unsigned long long* tr = nullptr;   // per-step arrival / release times (workgroup 0 only)
-    int t = 0, w = 0;
-    unsigned long long seg[4] = {0, 0, 0, 0}, ts = 0;
-};
-#ifdef PSGLA_STAMPS_SEG
-#define STAMP_SEG(st, i) do { const unsigned long long _n = stamp_now(); (st).seg[i] += _n - (st).ts; (st).ts = _n; } while (0)
-#define STAMP_START(st) do { (st).ts = stamp_now(); } while (0)
-#else
-#define STAMP_SEG(st, i) do { } while (0)
-#define STAMP_START(st) do { } while (0)
-#endif
-__device__ __forceinline__ unsigned long long stamp_now() {
-#ifdef PSGLA_STAMPS
-    unsigned long long t;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
-    return t;
-#else
-    return 0;
-#endif
-}
-__device__ __forceinline__ void step_barrier(Stamps& st) {
-#ifdef PSGLA_STAMPS
-    const unsigned long long t1 = stamp_now();
-    st.work += t1 - st.t0;
-    lds_barrier();
-    st.t0 = stamp_now();
-    st.wait += st.t0 - t1;
-    if (st.tr && (threadIdx.x & 63) == 0) {
-        st.tr[((size_t)st.t * 16 + st.w) * 2] = t1;
-        st.tr[((size_t)st.t * 16 + st.w) * 2 + 1] = st.t0;
-    }
-    ++st.t;
-#else
-    (void)st;
-    lds_barrier();
-#endif
-}
-
-// ---- point-to-point pipeline synchronisation (P2P variant) ----
-// Instead of one workgroup barrier per step, every wave publishes its progress in LDS (prog[w] = T + 1
-// once step T's ring reads have landed and its ring writes are performed: s_waitcnt lgkmcnt(0) first),
-// and waits only for the waves whose data it reads (RAW: the producer reached step T) or whose slot it
-// overwrites (WAR: the consumer reached step T) -- every dependency of step T is on step T - 1 work, so
-// neighbours drift by at most about one step and nothing can deadlock.  Waves that have no shared LDS
-// work in a step publish at its end.  A wait is a bounded poll (s_sleep between polls); on a timeout
-// the pass stops waiting (p2p_fail, reported through arrive[1]) so the grid still drains.
-constexpr uint32_t P2P_SPIN_MAX = 1u << 17;
-// issue priorities of the roles in the P2P pipeline (the barrier pipeline: front 0, stages 1, back 3)
-#ifndef PSGLA_P2P_PRIO_FRONT
-#define PSGLA_P2P_PRIO_FRONT 3
-#endif
-#ifndef PSGLA_P2P_PRIO_STAGE
-#define PSGLA_P2P_PRIO_STAGE 1
-#endif
-#ifndef PSGLA_P2P_PRIO_BACK
-#define PSGLA_P2P_PRIO_BACK 2
-#endif
-template <bool P2P>
-__device__ __forceinline__ void p2p_wait(StreamShared& sh, int wv, int target) {
-    if constexpr (P2P) {
-        if (target <= 0) return;
-        const uint32_t tg = (uint32_t)target;
-        for (uint32_t spins = 0;; ++spins) {
-            const uint32_t v = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&sh.prog[wv]);
-            if (v >= tg) break;
-            if (spins >= P2P_SPIN_MAX || *(volatile uint32_t*)&sh.p2p_fail) {
-                *(volatile uint32_t*)&sh.p2p_fail = 1u;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        asm volatile("" ::: "memory");
-    } else {
-        (void)sh; (void)wv; (void)target;
-    }
-}
-// A wave's LDS operations are performed in issue order (LDS-only lgkmcnt retires in order), so a
-// progress word written after a step's ring writes / reads is seen only once they are performed: the
-// publish needs no wait, and a progress word read BEFORE a row's ring reads ("peek"), if it already
-// shows the producer's step, proves those reads saw the row -- the poll's latency overlaps them.
-template <bool P2P>
-__device__ __forceinline__ void p2p_publish(StreamShared& sh, int w, int value) {
-    if constexpr (P2P) {
-        asm volatile("" ::: "memory");
-        *(volatile uint32_t*)&sh.prog[w] = (uint32_t)value;
-        asm volatile("" ::: "memory");
-    } else {
-        (void)sh; (void)w; (void)value;
-    }
-}
-template <bool P2P>
-__device__ __forceinline__ uint32_t p2p_peek(StreamShared& sh, int wv) {
-    if constexpr (P2P) {
-        const uint32_t v = *(volatile uint32_t*)&sh.prog[wv];
-        asm volatile("" ::: "memory");
-        return v;
-    } else {
-        (void)sh; (void)wv;
-        return 0xFFFFFFFFu;
-    }
-}
-// true when a peeked progress word already satisfies `target` (wave-uniform)
-template <bool P2P>
-__device__ __forceinline__ bool p2p_ok(uint32_t peeked, int target) {
-    if constexpr (P2P) return target <= 0 || __builtin_amdgcn_readfirstlane(peeked) >= (uint32_t)target;
-    else return true;
-}
-// end of step T: the workgroup barrier (barrier pipelines) or, if not done mid-step, the publish (P2P)
-template <bool P2P>
-__device__ __forceinline__ void step_end(StreamShared& sh, Stamps& st, int w, int T, bool published) {
-    if constexpr (P2P) {
-        if (!published) p2p_publish<true>(sh, w, T + 1);
-        (void)st;
-    } else {
-        (void)sh; (void)w; (void)T; (void)published;
-        step_barrier(st);
-    }
-}
+// end of a pipeline step: the workgroup barrier (LDS drained, LDS-DMA loads stay in flight)
+__device__ __forceinline__ void step_barrier() { lds_barrier(); }
 
 struct StepInfo {
     bool acc, first, blockend, liveout, sample;
@@ -1099,10 +903,9 @@ __device__ __forceinline__ void stage_phase_b(const TvArgs& a, const StageRow& r
 // Segment edges (split mode): the first row of a segment has no row above (its primal
 // uses u0 = 0 above) and the last has no row below (its dual has no vertical difference);
 // the rel-err partial sums are flushed per segment (different segments may be different chains).
-template <bool EXACT, bool TRK, bool GEN, bool P2P>
+template <bool EXACT, bool TRK, bool GEN>
 __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, const RowMap& rm, int k, int n,
-                                           int nsteps, int Qk, int lane, int lastk, int nreal, bool core,
-                                           Stamps& stp) {
+                                           int nsteps, int Qk, int lane, int lastk, int nreal, bool core) {
     // GEN: the lane's columns change with the column segment of the row (row split over virtual
     // planes): lastk / nreal / core follow the primal row's segment; each row carries its lastk
     // to its dual (StageRow.lk)
@@ -1117,17 +920,6 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
     };
     const int Q = Qk;                    // rows this stage runs (the stream's, bottom-halo trimmed)
     const int tbeg = 1 + 3 * k;          // step of lookahead row 0
-    // P2P: this wave, the producer of ring k-1 (stage k-1; for k = 1 the front wave of the row) and the
-    // consumer of ring k (stage k+1; for k = n the back wave of the row)
-    const int wme = SP_FRONT + k - 1;
-    auto raw_wave = [&](int j) { return k == 1 ? (j & 3) : wme - 1; };   // wrote ring k-1 row j
-    auto war_wave = [&](int i) { return k < n ? wme + 1 : SP_FRONT + n + ((i - 2) & 1); };  // read row i - 2
-    auto wait_raw = [&](int j) {          // before reading ring k-1 row j (step T = tbeg + j)
-        p2p_wait<P2P>(sh, raw_wave(j), tbeg + j);
-    };
-    auto wait_war = [&](int i, int T) {   // before writing ring k row i (its slot's previous row i - 2)
-        if (i - 2 >= 0) p2p_wait<P2P>(sh, war_wave(i), T);
-    };
     StageRow RA, RB, RC;
     const float zero[CPL] = {0.f, 0.f, 0.f, 0.f};
     float lsd = 0.f, lsn = 0.f;          // rel-err partial sums of segment sacc (core rows)
@@ -1152,7 +944,7 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
         if (TRK && j >= qc0 && j < qc1) { lsd += rd; lsn += rn; }
     };
     int t = 0;
-    for (; t < tbeg; ++t) step_end<P2P>(sh, stp, wme, t, false);
+    for (; t < tbeg; ++t) step_barrier();
     auto load_row = [&](int j, float4& X2, float4& U0, float4& U1, float4& YY) {
         const int sl = j & 1;
         X2 = sh.x2[k - 1][sl][lane];
@@ -1169,36 +961,22 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
     // rows 0 and 1: primal update only (segments hold >= 2 rows: row 1 never starts one)
     {
         float4 X2, U0, U1, YY;
-        wait_raw(0);
         load_row(0, X2, U0, U1, YY);
-        p2p_publish<P2P>(sh, wme, tbeg + 1);
         primal(0, X2, U0, U1, YY, zero, RA);
-        step_end<P2P>(sh, stp, wme, tbeg, true);
-        wait_raw(1);
+        step_barrier();
         load_row(1, X2, U0, U1, YY);
-        p2p_publish<P2P>(sh, wme, tbeg + 2);
         primal(1, X2, U0, U1, YY, RA.u0, RB);
-        step_end<P2P>(sh, stp, wme, tbeg + 1, true);
+        step_barrier();
         t += 2;
     }
     // middle rows j = 2..Q-1: dual update of row j-2 (p2) with z of row j-1 (p1), then primal of j
     auto middle = [&](int j, StageRow& p2, StageRow& p1, StageRow& cur) {
         float4 X2, U0, U1, YY;
-        const int T = tbeg + j;
-        // P2P: both progress words peeked ahead of the ring reads; checked where they matter
-        const uint32_t pk_raw = p2p_peek<P2P>(sh, raw_wave(j));
-        const uint32_t pk_war = p2p_peek<P2P>(sh, war_wave(j - 2));
         load_row(j, X2, U0, U1, YY);
         float un0[CPL], un1[CPL];
         if (!fprev) stage_phase_b<EXACT, true, GEN>(a, p2, p1.z, GEN ? p2.lk : lastk, un0, un1);
         else stage_phase_b<EXACT, false, GEN>(a, p2, zero, GEN ? p2.lk : lastk, un0, un1);   // row j-2 ends a segment
-        if (!p2p_ok<P2P>(pk_war, j - 4 >= 0 ? T : 0)) wait_war(j - 2, T);
         store_row(j - 2, p2, un0, un1);
-        if (!p2p_ok<P2P>(pk_raw, T)) {       // rare: the row was not there yet -- wait, read it again
-            wait_raw(j);
-            load_row(j, X2, U0, U1, YY);
-        }
-        p2p_publish<P2P>(sh, wme, T + 1);
         const bool fj = j == nb;
         if (fj) {                       // row j starts a new segment (split mode only)
             flush();
@@ -1210,7 +988,7 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
             primal(j, X2, U0, U1, YY, p1.u0, cur);
         }
         fprev = fj;
-        step_end<P2P>(sh, stp, wme, tbeg + j, true);
+        step_barrier();
     };
     int j = 2;
     for (; j + 2 < Q; j += 3) {
@@ -1224,13 +1002,11 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
     auto finish = [&](StageRow& r2, StageRow& r1) {
         float un0[CPL], un1[CPL];
         stage_phase_b<EXACT, true, GEN>(a, r2, r1.z, GEN ? r2.lk : lastk, un0, un1);
-        wait_war(Q - 2, tbeg + Q);
         store_row(Q - 2, r2, un0, un1);
-        step_end<P2P>(sh, stp, wme, tbeg + Q, false);
+        step_barrier();
         stage_phase_b<EXACT, false, GEN>(a, r1, zero, GEN ? r1.lk : lastk, un0, un1);
-        wait_war(Q - 1, tbeg + Q + 1);
         store_row(Q - 1, r1, un0, un1);
-        step_end<P2P>(sh, stp, wme, tbeg + Q + 1, false);
+        step_barrier();
     };
     const int rem = Q - j;              // 0, 1 or 2 middle rows left
     if (rem == 0) {
@@ -1244,7 +1020,7 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
         finish(RC, RA);
     }
     t += rem + 2;
-    for (; t < nsteps; ++t) step_end<P2P>(sh, stp, wme, t, false);
+    for (; t < nsteps; ++t) step_barrier();
     flush();
 }
 
@@ -1253,16 +1029,11 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
 // pass and the rare early-stop recompute, each with its own register allocation.
 // GEN: the row pitch is not the image width (rows padded: W % 4 != 0) -- the last-column, norm
 // and noise-window handling of such rows, compiled only into the kernels that need it
-template <bool EXACT, bool ALPHA1, bool GEN, bool P2P>
+template <bool EXACT, bool ALPHA1, bool GEN>
 __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, const RowMap& rm, const int n,
-                                            const bool track, const long long step, const bool fresh, Stamps& stp) {
+                                            const bool track, const long long step, const bool fresh) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (scalar branches)
-    if constexpr (P2P) {                                   // progress counters of this pass start at 0
-        if (threadIdx.x < 16) sh.prog[threadIdx.x] = 0u;
-        if (threadIdx.x == 0) sh.p2p_fail = 0u;
-        lds_barrier();
-    }
     const int H = a.H, W = a.W, C = a.C;
     const int L = a.ldw;                                   // row pitch (memory); W: the image's width
     const size_t HW = (size_t)H * L;                       // plane pitch
@@ -1315,15 +1086,11 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         cursor_init(rm, rc_dma, min(fw, Q - 1));
         // part `part` of the loads of stream row q: 0 = X, 1 = y, 2 = u2 (two halves), 3 = mask (+ x2)
         auto front_issue = [&](int part, int q, const RowCursor& rc) {
-#ifdef PSGLA_ABL_NOLOAD
-            return;     // diagnostic timing build only
-#endif
             const int rr = min(rc.r, H - 1);
             const int bi = (q >> 2) & 1;
             const SegGeo g = seg_geo<GEN>(a, rc.p);
             const int gjr = GEN ? min(g.f0 + CPL * lane, L - CPL) : gjc;
             const int bb = g.rp / C;
-#ifndef PSGLA_STREAM_SADDR
             // 64-bit per-lane addresses (default; the SGPR-base form, -DPSGLA_STREAM_SADDR, measured +12 %:
             // this kernel's row cursor sits in VGPRs, so each DMA pays two readfirstlane + 5 wait states)
             const size_t base = plane_off(g.rp) + (size_t)rr * L + gjr;
@@ -1339,36 +1106,13 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                 if (!ALPHA1) glds16(x2in + base, &sh.fst[fw][bi][4][0]);
                 glds4(a.mask + (size_t)bb * a.m_cs + (size_t)rr * L + gjr, &sh.fmk[fw][bi][0]);
             }
-#else
-            // the row's base in SGPRs (saddr), the lane's column as a 32-bit byte offset
-            const size_t rb = plane_off(g.rp) + (size_t)rr * L;
-            const uint32_t vo = (uint32_t)gjr * 4u;
-            if (part == 0) {
-                sglds16(xin + rb, vo, &sh.fst[fw][bi][0][0]);
-            } else if (part == 1) {
-                sglds16(a.yobs + (size_t)bb * a.y_cs + (size_t)(g.rp - bb * C) * HW + (size_t)rr * L, vo,
-                        &sh.fst[fw][bi][1][0]);
-            } else if (part == 2) {
-                sglds16(u2in + 2 * rb, 2u * vo, &sh.fst[fw][bi][2][0]);
-                sglds16(u2in + 2 * rb + 4, 2u * vo, &sh.fst[fw][bi][3][0]);
-            } else {
-                if (!ALPHA1) sglds16(x2in + rb, vo, &sh.fst[fw][bi][4][0]);
-                sglds4(a.mask + (size_t)bb * a.m_cs + (size_t)rr * L, (uint32_t)gjr, &sh.fmk[fw][bi][0]);
-            }
-#endif
         };
         // row fw's loads up front; afterwards the loads of row q + 4 are issued one part per
         // phase of row q (into the buffer of row q - 4, consumed before phase 0 of row q), so
         // their issue cost is spread over four steps
         for (int part = 0; part < 4; ++part) front_issue(part, fw, rc_dma);
         cursor_advance(rm, rc_dma, min(4, max(0, Q - 1 - fw)));
-#ifdef PSGLA_ABL_NOFRONT
-        for (int t = 0; t < nsteps; ++t) step_barrier(stp);   // diagnostic timing build only
-        if (nsteps >= 0) return;
-#endif
-        if (P2P) __builtin_amdgcn_s_setprio(PSGLA_P2P_PRIO_FRONT);
         for (int t = 0; t < nsteps; ++t) {
-                bool pub = false;
                 // ======================= FRONT =======================
                 const int p = (t + 4 - fw) & 3;
                 const int q = t - p;
@@ -1411,12 +1155,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                             zn0 = r4[0]; zn1 = r4[1]; zn2 = r4[2]; zn3 = r4[3];
                         }
                     } else {
-                        STAMP_START(stp);
-                        // P2P: the slots this phase overwrites (see below), peeked ahead
-                        const uint32_t pk_s1 = p2p_peek<P2P>(sh, SP_FRONT);
-                        const uint32_t pk_sn = p2p_peek<P2P>(sh, SP_FRONT + n - 1);
                         wait_vm<ALPHA1 ? 4 : 4>();   // row q's loads landed; parts 0-2 of row q + 4 may fly
-                        STAMP_SEG(stp, 0);
                         const int bi = (q >> 2) & 1;
                         const float4 fX = sh.fst[fw][bi][0][lane];
                         const float4 fYo = sh.fst[fw][bi][1][lane];
@@ -1446,30 +1185,17 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                         else x2s = ALPHA1 ? fX : fXS;
                         if (!okf) x2s = zero4;
                         const int s0 = q & 1;
-                        STAMP_SEG(stp, 1);
-                        // P2P: ring 0 slot (previous row q - 2, read by stage 1 at step t - 1) and Y-ring
-                        // slot (row q - 32: read by the stages up to step t - 4, by the back at t - 1)
-                        if (!p2p_ok<P2P>(pk_s1, t)) p2p_wait<P2P>(sh, SP_FRONT, t);
-                        if (!p2p_ok<P2P>(pk_sn, t - 33 + 3 * n)) p2p_wait<P2P>(sh, SP_FRONT + n - 1, t - 33 + 3 * n);
-                        if (!ALPHA1) {
-                            p2p_wait<P2P>(sh, SP_FRONT + n, t);
-                            p2p_wait<P2P>(sh, SP_FRONT + n + 1, t);
-                        }
                         sh.x2[0][s0][lane] = x2s;
                         sh.u0[0][s0][lane] = fresh ? zero4 : make_float4(fU0.x, fU0.z, fU1.x, fU1.z);
                         sh.u1[0][s0][lane] = fresh ? zero4 : make_float4(fU0.y, fU0.w, fU1.y, fU1.w);
                         sh.y[q & (SP_YRING - 1)][lane] = Y4;
-                        p2p_publish<P2P>(sh, fw, t + 1);
-                        pub = true;
-                        STAMP_SEG(stp, 2);
-                        // the wave's next rows: noise row q + 4, DMA of row q + 8... issued as q + 4
+                            // the wave's next rows: noise row q + 4, DMA of row q + 8... issued as q + 4
                         front_issue(3, q + 4, rc_dma);
                         cursor_advance(rm, rc_cur, 4);
                         if (q + 8 < Q) cursor_advance(rm, rc_dma, 4);
-                        STAMP_SEG(stp, 3);
                     }
                 }
-            step_end<P2P>(sh, stp, fw, t, pub);
+            step_barrier();
         }
     } else if (role == 1) {
         // ---------------- STAGE (one inner TV iteration per wave) ----------------
@@ -1478,25 +1204,19 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         // select: the DPP shift feeds 0 at lane 0 and TV keeps those dual components exactly 0.
         const int lastk = W - 1 - gj0;                    // in 0..3 on the lane holding column W-1
         const int nreal = min(CPL, max(0, W - gj0));      // real (non-pitch-padding) columns of the lane
-        if (P2P) __builtin_amdgcn_s_setprio(PSGLA_P2P_PRIO_STAGE);
-        else __builtin_amdgcn_s_setprio(1);
+        __builtin_amdgcn_s_setprio(1);
         const int qk = stage_rows(k_st);
-        if (trk) stage_loop<EXACT, true, GEN, P2P>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core, stp);
-        else stage_loop<EXACT, false, GEN, P2P>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core, stp);
+        if (trk) stage_loop<EXACT, true, GEN>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core);
+        else stage_loop<EXACT, false, GEN>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core);
     } else if (role == 3) {
-        for (int t = 0; t < nsteps; ++t) step_end<P2P>(sh, stp, w, t, false);
+        for (int t = 0; t < nsteps; ++t) step_barrier();
     } else {
-#ifdef PSGLA_ABL_NOBACK
-        for (int t = 0; t < nsteps; ++t) step_barrier(stp);   // diagnostic timing build only
-        if (nsteps >= 0) return;
-#endif
         // ---------------- BACK state ----------------
         const int bw = w - SP_FRONT - n;                   // back wave id (stream rows q % 2 == bw)
         // issue priority: back > stages > front.  The back waves are the youngest of the
         // workgroup (lowest age priority) yet close every step (its last arrivals, measured);
         // raising them, then the stages, cut the step by 9 % (A/B).
-        if (P2P) __builtin_amdgcn_s_setprio(PSGLA_P2P_PRIO_BACK);
-        else __builtin_amdgcn_s_setprio(3);
+        __builtin_amdgcn_s_setprio(3);
         const StepInfo si = step_info(a, step, a.mean[par_out]);
         const float* mean_in = a.mean[par_in];
         const float* sq_in = a.sq[par_in];
@@ -1506,23 +1226,14 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         cursor_init(rm, rc_cur, min(bw, Q - 1));
         cursor_init(rm, rc_dma, min(bw, Q - 1));
         auto back_issue = [&](int q, const RowCursor& rc) {
-#ifdef PSGLA_ABL_NOLOAD
-            return;     // diagnostic timing build only
-#endif
             if (need_prev) {
                 const int rr = min(rc.r, H - 1);
                 const int bi = (q >> 1) & 1;
                 const SegGeo g = seg_geo<GEN>(a, rc.p);
                 const int gjr = GEN ? min(g.f0 + CPL * lane, L - CPL) : gjc;
-#ifndef PSGLA_STREAM_SADDR
                 const size_t base = plane_off(g.rp) + (size_t)rr * L + gjr;
                 glds16(mean_in + base, &sh.bst[bw][bi][0][0]);
                 glds16(sq_in + base, &sh.bst[bw][bi][1][0]);
-#else
-                const size_t rb = plane_off(g.rp) + (size_t)rr * L;
-                sglds16(mean_in + rb, (uint32_t)gjr * 4u, &sh.bst[bw][bi][0][0]);
-                sglds16(sq_in + rb, (uint32_t)gjr * 4u, &sh.bst[bw][bi][1][0]);
-#endif
             }
         };
         // vector-memory stores per core row (all lanes of a wave store together; lane 0 is core)
@@ -1534,7 +1245,6 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         float4 hM = zero4, hQ = zero4, hX = zero4;
         auto flush_held = [&]() {
             if (!(GEN ? hcore : core)) return;
-#ifndef PSGLA_STREAM_SADDR
             if (si.acc) {
                 if (si.blockend) {
                     st_nt(a.blocks + (size_t)si.blk * BE + h_base, hM);
@@ -1545,18 +1255,6 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                 }
             }
             if (si.sample) st_nt(a.samples + (size_t)si.sidx * BE + h_base, hX);
-#else
-            if (si.acc) {
-                if (si.blockend) {
-                    sgst16(a.blocks + (size_t)si.blk * BE + h_base, h_vo, hM);
-                    sgst16(a.blocks2 + (size_t)si.blk * BE + h_base, h_vo, hQ);
-                } else if (si.liveout) {
-                    sgst16(a.mean[par_out] + h_base, h_vo, hM);
-                    sgst16(a.sq[par_out] + h_base, h_vo, hQ);
-                }
-            }
-            if (si.sample) sgst16(a.samples + (size_t)si.sidx * BE + h_base, h_vo, hX);
-#endif
         };
         // mean / sq rows are LDS-DMA'd two of the wave's rows ahead (4 stream rows); c1 / c2 =
         // vector-memory ops issued after the DMA of the wave's next / next-but-one row
@@ -1565,22 +1263,14 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         back_issue(bw + 2, rc_dma);
         int c1 = 2, c2 = 0;
         for (int t = 0; t < nsteps; ++t) {
-                bool pub = false;
                 // ======================= BACK =======================
                 const int q = t - 4 - 3 * n;
                 if (q >= 0 && q < Qb && (q & 1) == bw) {
                     const int sl = q & 1;
-                    // stage n wrote ring n row q at step t - 1 (P2P: peeked ahead of the reads)
-                    const uint32_t pk = p2p_peek<P2P>(sh, SP_FRONT + n - 1);
-                    float4 X2 = sh.x2[n][sl][lane];
-                    float4 U0 = sh.u0[n][sl][lane];
-                    float4 U1 = sh.u1[n][sl][lane];
-                    if (!p2p_ok<P2P>(pk, t)) {
-                        p2p_wait<P2P>(sh, SP_FRONT + n - 1, t);
-                        X2 = sh.x2[n][sl][lane];
-                        U0 = sh.u0[n][sl][lane];
-                        U1 = sh.u1[n][sl][lane];
-                    }
+                    // stage n wrote ring n row q at step t - 1
+                    const float4 X2 = sh.x2[n][sl][lane];
+                    const float4 U0 = sh.u0[n][sl][lane];
+                    const float4 U1 = sh.u1[n][sl][lane];
                     float4 Xo = X2;
                     if (!ALPHA1) {
                         const float4 YY = sh.y[q & (SP_YRING - 1)][lane];
@@ -1618,8 +1308,6 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                     // all LDS reads of this row (ring + staging) done before the staging
                     // buffer is re-targeted by the next DMA
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    p2p_publish<P2P>(sh, SP_FRONT + n + bw, t + 1);
-                    pub = true;
                     const RowCursor rc = rc_cur;
                     cursor_advance(rm, rc_cur, 2);
                     if (q + 4 < Q) cursor_advance(rm, rc_dma, 2);
@@ -1635,7 +1323,6 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                     const SegGeo gr = seg_geo<GEN>(a, rc.p);
                     const int gjr = GEN ? gr.f0 + CPL * lane : gj0;
                     const bool corer = GEN ? (gjr < W && gjr >= gr.cc0 && gjr < gr.cc1) : core;
-#ifndef PSGLA_STREAM_SADDR
                     if (rowcore && corer) {
                         const size_t base = plane_off(gr.rp) + (size_t)rc.r * L + gjr;
                         st_nt(a.x[par_out] + base, Xo);
@@ -1646,45 +1333,22 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
                         // the accumulator / sample stores go out in the wave's next (idle) step
                         h_base = base; hM = M4; hQ = Q4; hX = Xo;
                     }
-#else
-                    const size_t rb = plane_off(gr.rp) + (size_t)rc.r * L;   // the row's base (uniform)
-                    const uint32_t vo = (uint32_t)gjr * 4u;
-                    if (rowcore) { h_base = rb; h_vo = vo; }
-                    if (rowcore && corer) {
-                        sgst16(a.x[par_out] + rb, vo, Xo);
-                        sgst16(a.u2[par_out] + 2 * rb, 2u * vo, make_float4(U0.x, U1.x, U0.y, U1.y));
-                        sgst16(a.u2[par_out] + 2 * rb + 4, 2u * vo, make_float4(U0.z, U1.z, U0.w, U1.w));
-                        if (!ALPHA1) sgst16(a.x2[par_out] + rb, vo, X2);
-                        // the accumulator / sample stores go out in the wave's next (idle) step
-                        hM = M4; hQ = Q4; hX = Xo;
-                    }
-#endif
                     hold = rowcore;
                     if (GEN) hcore = corer;
                 } else if (hold) {
                     flush_held();
                     hold = false;
                 }
-            step_end<P2P>(sh, stp, SP_FRONT + n + bw, t, pub);
+            step_barrier();
         }
         if (hold) flush_held();
     }
 
-#ifdef PSGLA_STAMPS
-    if (a.stamps && lane == 0) {
-        a.stamps[((size_t)blockIdx.x * 16 + w) * 2] = stp.work;
-        a.stamps[((size_t)blockIdx.x * 16 + w) * 2 + 1] = stp.wait;
-        if (w < SP_FRONT) {
-            unsigned long long* sg = a.stamps + (size_t)gridDim.x * 32 + (size_t)nsteps * 32 + ((size_t)blockIdx.x * 4 + w) * 4;
-            for (int i = 0; i < 4; ++i) sg[i] = stp.seg[i];
-        }
-    }
-#endif
     // rel_err partial sums of this stream -> global, per segment's chain (deepinv's
     // early-stop test, per chain); the tracking stages wrote sh.red[segment][k - 1]
 }
 
-template <bool EXACT, bool ALPHA1, bool GEN, bool P2P>
+template <bool EXACT, bool ALPHA1, bool GEN>
 __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     __shared__ StreamShared sh;
     __shared__ int s_stop[MAXG];
@@ -1692,20 +1356,10 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     const int C = a.C;
     const long long step = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
     const bool fresh = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
-    Stamps stp;
-    stp.t0 = stamp_now();
-#ifdef PSGLA_STAMPS
-    stp.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    stp.tr = (a.stamps && blockIdx.x == 0) ? a.stamps + (size_t)gridDim.x * 32 : nullptr;
-#endif
     {
         RowMap rm;
         build_rowmap(a, blockIdx.x, rm);
-        stream_pass<EXACT, ALPHA1, GEN, P2P>(a, sh, rm, a.n_tv, true, step, fresh, stp);
-        if (P2P) {
-            lds_barrier();
-            if (threadIdx.x == 0 && sh.p2p_fail) atomicOr(a.arrive + 1, 1);   // diagnostic: a wait timed out
-        }
+        stream_pass<EXACT, ALPHA1, GEN>(a, sh, rm, a.n_tv, true, step, fresh);
         if (!a.fin_inline) return;        // main-pass-only launch (kernel timing): no side effects
         // rel_err partial sums of this stream -> global, per segment's chain (deepinv's
         // early-stop test, per chain); the tracking stages wrote sh.red[segment][k - 1]
@@ -1778,7 +1432,7 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
         RowMap rm;
         plane_rowmap(a.H, item, rm);                 // the virtual plane (plane, column segment)
         const int nstop = __builtin_amdgcn_readfirstlane(s_stop[plane / C]);
-        stream_pass<EXACT, ALPHA1, GEN, P2P>(a, sh, rm, nstop, false, step, fresh, stp);
+        stream_pass<EXACT, ALPHA1, GEN>(a, sh, rm, nstop, false, step, fresh);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < a.B * a.n_tv * 2; i += blockDim.x) a.norms[i] = 0.0;
@@ -1786,6 +1440,530 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
         *a.arrive = 0;
         if (a.fresh_dev) *a.fresh_dev = 0;
         if (a.advance_step && a.d_step) *a.d_step = *a.d_step + 1;   // (re-read: the start-of-kernel value measured +0.5 % here)
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Row-PAIR pipeline (tv_pair_kernel): the fused PSGLA + TV step with TWO rows per pipeline step.
+//
+// The row-stream pipeline above spends ~1,660 cycles per row step for ~780 cycles of VALU work per
+// SIMD: every wave's per-step chain (LDS read -> dependent VALU -> LDS write) is exposed once per row
+// and the SIMDs idle between the bursts.  Here every role handles a row PAIR
+// per step -- two independent dependency chains per wave, half the steps per row -- and the steps are
+// split into two phases so that each LDS ring needs ONE slot of two rows (two-slot rings of row
+// pairs do not fit in 160 KB):
+//   W-phase  stage k: dual update of the row pair (a-3, a-2) (all inputs in registers), written to
+//                     ring k; front: its finished pair written to ring 0 and to the Y ring
+//   barrier
+//   C-phase  stage k: reads ring k-1 = rows (a, a+1) (written in this step's W-phase), primal update
+//                     of both; front / back: noise, data term, loads, accumulators, stores
+//   barrier
+// with a = 2t - 3k + 3 for stage k at step t (stage k+1 trails stage k by 3 rows; the front hands
+// rows (2t, 2t+1) to stage 1 at step t; the back takes rows (2t - 3n, 2t - 3n + 1) from ring n).
+// A ring slot written in W_t is read in C_t and next written in W_{t+1}, after the C_t barrier.
+// The per-element arithmetic is the row stream's (stage_phase_a / stage_phase_b, the same data term
+// and accumulators): exact mode is bit-identical to the oracle, fast mode to the fast row stream.
+// Shape: one 256-column window (W <= 256, W % 4 == 0, rows unpadded), alpha == 1 (X == x2); the same
+// row split over the CUs (build_rowmap), per-chain early stop and in-kernel finalisation.
+// ---------------------------------------------------------------------------------------
+constexpr int PR_YRING = 30;      // Y rows kept from the front (step r/2) to the last stage (step (r+27)/2)
+constexpr int PR_ZRING = 4;       // noise of 4 row pairs (written 2 steps before the front consumes it)
+constexpr int PR_NZ = 3;          // stage waves 1..3 also generate the Langevin noise (n_tv >= 3)
+constexpr int PR_T0 = -6;         // first step: noise of pair 0 starts at step -5
+
+struct PairShared {
+    float4 x2[SP_MAXST + 1][2][WAVE];     // ring k (k = 0: front): the row pair handed to stage k + 1
+    float4 u0[SP_MAXST + 1][2][WAVE];
+    float4 u1[SP_MAXST + 1][2][WAVE];
+    float4 y[PR_YRING][WAVE];             // Y rows (prox anchor), by stream row % 30
+    float4 z[PR_ZRING][2][WAVE];          // Langevin noise Z of a row pair, by pair % 4
+    float4 fst[SP_FRONT][2][4][WAVE];     // front LDS-DMA staging of its next pair: X, y, u2 lo, u2 hi
+    uint32_t fmk[SP_FRONT][2][WAVE];      // mask bytes (4 columns per lane)
+    float4 bst[SP_BACK][2][2][2][WAVE];   // back staging [buffer][row][mean, sq]
+    float red[SP_MAXSEG][SP_MAXST][2];
+};
+
+__device__ __forceinline__ int pr_yslot(int r) { return (r + 32 * PR_YRING) % PR_YRING; }   // r >= -960
+
+// stream row q starts a segment (the stream's first row, or a plane start inside a split range)
+__device__ __forceinline__ bool seg_start(const RowMap& m, int q) {
+    return q == 0 || (m.ns > 1 && q == m.q1) || (m.ns > 2 && q == m.q2) || (m.ns > 3 && q == m.q3);
+}
+
+// Langevin noise of stream row q (Philox of the lane's quad; W % 4 == 0, so a lane's 4 columns are one quad
+// of the chain's C*H*W image) -- in three pieces: Philox, Box-Muller of outputs 0-1, of outputs 2-3.  The
+// state is a lane's 4 words, Philox outputs first, then the normals' bits in place.
+__device__ __forceinline__ void noise_philox(const TvArgs& a, const RowMap& rm, int q, long long step, int gj0,
+                                             uint32_t (&nz)[4]) {
+    RowCursor c;
+    cursor_init(rm, c, min(max(q, 0), rm.Q - 1));
+    const int bb = c.p / a.C, cc = c.p - bb * a.C;
+    const size_t e = ((size_t)cc * a.H + c.r) * a.W + gj0;
+    uint32_t c0 = (uint32_t)(e >> 2), c1 = (uint32_t)step, c2 = TAG_LANGEVIN, c3 = (uint32_t)(a.seed >> 32);
+    philox4x32_10(c0, c1, c2, c3, (uint32_t)a.seed, (uint32_t)(a.chain0 + bb));
+    nz[0] = c0; nz[1] = c1; nz[2] = c2; nz[3] = c3;
+}
+template <int h>
+__device__ __forceinline__ void noise_bm(uint32_t (&nz)[4]) {
+    float z0, z1;
+    box_muller(nz[2 * h], nz[2 * h + 1], z0, z1);
+    nz[2 * h] = __float_as_uint(z0);
+    nz[2 * h + 1] = __float_as_uint(z1);
+}
+
+// Stage k over the steps [T0, T1): see the section comment for the schedule.  Three row states
+// rotate (prev | pair): after C_t, `prev` holds row a-1 and the pair rows a, a+1; the next W-phase
+// duals rows a-1 and a (z of a and a+1 known) and the pair's second row becomes `prev`.  Stages
+// 1..PR_NZ also generate the noise of one row pair every PR_NZ steps (a piece per phase).
+template <bool EXACT, bool TRK>
+__device__ __forceinline__ void pair_stage(const TvArgs& a, PairShared& sh, const RowMap& rm, int k, int T0,
+                                           int T1, int lane, int lastk, bool core, long long stepi) {
+    const int Q = rm.Q;
+    const int qc0 = rm.htop, qc1 = Q - rm.hbot;
+    const float zero[CPL] = {0.f, 0.f, 0.f, 0.f};
+    StageRow R0, R1, R2;
+    float lsd = 0.f, lsn = 0.f;          // rel-err partial sums of segment sacc (core rows)
+    int sacc = 0;
+    const bool nzw = k <= PR_NZ;         // a noise wave
+    uint32_t nza[4] = {0u, 0u, 0u, 0u}, nzb[4] = {0u, 0u, 0u, 0u};
+    auto flush = [&]() __attribute__((always_inline)) {
+        if (TRK) {
+            float d = wave_sum(core ? lsd : 0.f);
+            const float q = wave_sum(core ? lsn : 0.f);
+            if (!EXACT) d *= a.rho * a.rho;          // fast sums hold (x - x2_prev)^2
+            if (lane == 0) { sh.red[sacc][k - 1][0] = d; sh.red[sacc][k - 1][1] = q; }
+            lsd = 0.f; lsn = 0.f;
+        }
+    };
+    // dual update of row r (state d, z of the row below in zb) -> ring k slot s
+    auto dual = [&](int r, const StageRow& d, const StageRow& zb, int s) __attribute__((always_inline)) {
+        if (r < 0 || r >= Q) return;
+        float un0[CPL], un1[CPL];
+        if (r + 1 < Q && !seg_start(rm, r + 1)) stage_phase_b<EXACT, true>(a, d, zb.z, lastk, un0, un1);
+        else stage_phase_b<EXACT, false>(a, d, zero, lastk, un0, un1);   // the segment's last row
+        sh.x2[k][s][lane] = make_float4(d.x2n[0], d.x2n[1], d.x2n[2], d.x2n[3]);
+        sh.u0[k][s][lane] = make_float4(un0[0], un0[1], un0[2], un0[3]);
+        sh.u1[k][s][lane] = make_float4(un1[0], un1[1], un1[2], un1[3]);
+    };
+    // primal update of row r from ring k-1 slot s (u0 of the row above in pa)
+    auto primal = [&](int r, const float4& X2, const float4& U0, const float4& U1, const float4& YY,
+                      const StageRow& pa, StageRow& o) __attribute__((always_inline)) {
+        if (r < 0 || r >= Q) return;
+        const bool fs = seg_start(rm, r);
+        if (TRK && fs && r > 0) { flush(); ++sacc; }
+        float rd = 0.f, rn = 0.f;
+        // u0 of the row above (none at a segment start); selected by value: two call sites fed
+        // `zero` / pa.u0 get merged over a pointer select into scratch memory
+        float pu[CPL];
+#pragma unroll
+        for (int kk = 0; kk < CPL; ++kk) pu[kk] = fs ? 0.f : pa.u0[kk];
+        stage_phase_a<EXACT, TRK>(a, X2, U0, U1, YY, pu, o, rd, rn);
+        if (TRK && r >= qc0 && r < qc1) { lsd += rd; lsn += rn; }
+    };
+    // noise duty (stage k <= PR_NZ): pair p = t + 5 - pi with p = k - 1 (mod PR_NZ), piece pi of 3 per phase:
+    //   pi 0: Philox of rows a / b (W / C), 1: Box-Muller 0-1, 2: Box-Muller 2-3, then Z of pair p to LDS
+    // (the row's state is picked at compile time: a runtime-selected array reference goes to scratch)
+    auto noise = [&](int t, auto phc) __attribute__((always_inline)) {
+        constexpr int ph = decltype(phc)::value;
+        if (!nzw) return;
+        const int pi = ((t + 5 - (k - 1)) % PR_NZ + PR_NZ) % PR_NZ;
+        const int p = t + 5 - pi;
+        if (p < 0 || 2 * p >= Q) return;
+        if constexpr (ph == 0) {
+            if (pi == 0) noise_philox(a, rm, 2 * p, stepi, CPL * lane, nza);
+            else if (pi == 1) noise_bm<0>(nza);
+            else noise_bm<1>(nza);
+        } else {
+            if (pi == 0) noise_philox(a, rm, 2 * p + 1, stepi, CPL * lane, nzb);
+            else if (pi == 1) noise_bm<0>(nzb);
+            else noise_bm<1>(nzb);
+        }
+        if (ph == 1 && pi == 2) {
+            sh.z[p & (PR_ZRING - 1)][0][lane] = make_float4(__uint_as_float(nza[0]), __uint_as_float(nza[1]),
+                                                            __uint_as_float(nza[2]), __uint_as_float(nza[3]));
+            sh.z[p & (PR_ZRING - 1)][1][lane] = make_float4(__uint_as_float(nzb[0]), __uint_as_float(nzb[1]),
+                                                            __uint_as_float(nzb[2]), __uint_as_float(nzb[3]));
+        }
+    };
+    // one step with the roles (prev P | pair A, B): W duals P (row a-3) and A (row a-2), C reads rows
+    // a, a+1 into P and A (the new pair; B becomes prev)
+    auto step = [&](int t, StageRow& P, StageRow& A, StageRow& B) __attribute__((always_inline)) {
+        const int r = 2 * t - 3 * k + 3;
+        dual(r - 3, P, A, 0);
+        dual(r - 2, A, B, 1);
+        noise(t, std::integral_constant<int, 0>());
+        lds_barrier();
+        if (r + 1 >= 0 && r < Q) {
+            const float4 X2a = sh.x2[k - 1][0][lane], U0a = sh.u0[k - 1][0][lane], U1a = sh.u1[k - 1][0][lane];
+            const float4 X2b = sh.x2[k - 1][1][lane], U0b = sh.u0[k - 1][1][lane], U1b = sh.u1[k - 1][1][lane];
+            const float4 Ya = sh.y[pr_yslot(r)][lane], Yb = sh.y[pr_yslot(r + 1)][lane];
+            primal(r, X2a, U0a, U1a, Ya, B, P);
+            primal(r + 1, X2b, U0b, U1b, Yb, P, A);
+        }
+        noise(t, std::integral_constant<int, 1>());
+        lds_barrier();
+    };
+    int t = T0;
+    for (; t + 2 < T1; t += 3) {
+        step(t, R0, R1, R2);
+        step(t + 1, R2, R0, R1);
+        step(t + 2, R1, R2, R0);
+    }
+    if (t < T1) step(t, R0, R1, R2);
+    if (t + 1 < T1) step(t + 1, R2, R0, R1);
+    flush();
+}
+
+template <bool EXACT>
+__device__ __forceinline__ void pair_pass(const TvArgs& a, PairShared& sh, const RowMap& rm, const int n,
+                                          const bool track, const long long step, const bool fresh) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (scalar branches)
+    const int H = a.H, W = a.W, C = a.C;
+    const size_t HW = (size_t)H * W;
+    const size_t BE = (size_t)a.B * C * HW;
+    const int par_in = (int)(step & 1), par_out = (int)((step + 1) & 1);
+    const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int Q = rm.Q;
+    const int qc0 = rm.htop, qc1 = Q - rm.hbot;          // core stream rows
+    const int gj0 = CPL * lane;
+    const bool lane_ok = gj0 < W;
+    const int gjc = min(gj0, W - CPL);                    // load column (every lane in bounds)
+    // steps T0 .. T1-1: noise of pair p from step p-5, the front's data term of pair p in step p-1, the
+    // hand-over in W_p; the back takes rows (2t - 3n, 2t - 3n + 1) at step t and finishes their stores
+    // in W_{t+2}
+    const int T0 = PR_T0;
+    const int T1 = (qc1 - 2 + 3 * n + 1) / 2 + 3;
+    const int role = (w < SP_FRONT) ? 0 : (w < SP_FRONT + n ? 1 : (w < SP_FRONT + n + SP_BACK ? 2 : 3));
+    const int k_st = w - SP_FRONT + 1;
+    const bool trk = track && role == 1 && (k_st - 1) >= 2 && (k_st - 1) <= n - 2;
+    // (plane, plane row) of stream row q, q clamped into the stream
+    auto locate = [&](int q, int& pl, int& rr) __attribute__((always_inline)) {
+        RowCursor c;
+        cursor_init(rm, c, min(max(q, 0), Q - 1));
+        pl = c.p;
+        rr = c.r;
+    };
+
+    if (role == 0) {
+        // ---------------- FRONT: pairs p = f, f + 4, ... ----------------
+        // With phs = (t - f) & 3 and p = t + 4 - phs, step t of front wave f does
+        //   phs 0  W: hand pair t to stage 1 (ring 0, Y ring); DMA piece B of pair p;  C: DMA piece C of pair p
+        //   phs 3  W: pair p's loads landed, data term of row a;  C: data term of row b, DMA piece A of pair p + 4
+        // (pieces: A = row a's X, y, u2 lo; B = row a's u2 hi, mask and row b's X; C = row b's y, u2, mask:
+        // each issued once its staging slot has been read, 2.5 - 3 steps before the data term).
+        const int f = w;
+        const float* xin = a.x[par_in];
+        const float* u2in = a.u2[par_in];
+        // LDS-DMA of part `part` (0 X, 1 y, 2 u2 lo, 3 u2 hi, 4 mask) of stream row q into staging slot i
+        auto dma = [&](int q, int i, int part) __attribute__((always_inline)) {
+            int pl, rr;
+            locate(q, pl, rr);
+            const int bb = pl / C;
+            const size_t base = (size_t)pl * HW + (size_t)rr * W + gjc;
+            if (part == 0) glds16(xin + base, &sh.fst[f][i][0][0]);
+            else if (part == 1)
+                glds16(a.yobs + (size_t)bb * a.y_cs + (size_t)(pl - bb * C) * HW + (size_t)rr * W + gjc,
+                       &sh.fst[f][i][1][0]);
+            else if (part == 2) glds16(u2in + 2 * base, &sh.fst[f][i][2][0]);
+            else if (part == 3) glds16(u2in + 2 * base + 4, &sh.fst[f][i][3][0]);
+            else glds4(a.mask + (size_t)bb * a.m_cs + (size_t)rr * W + gjc, &sh.fmk[f][i][0]);
+        };
+        float4 oY[2], oX[2], oU0[2], oU1[2];               // pair p's ring-0 rows, handed over in W_p
+        for (int i = 0; i < 2; ++i) oY[i] = oX[i] = oU0[i] = oU1[i] = zero4;
+        auto data_term = [&](int p, int i) __attribute__((always_inline)) {
+            const float4 fX = sh.fst[f][i][0][lane];
+            const float4 fYo = sh.fst[f][i][1][lane];
+            const float4 fU0 = sh.fst[f][i][2][lane];
+            const float4 fU1 = sh.fst[f][i][3][lane];
+            const uint32_t fMw = sh.fmk[f][i][lane];
+            const float4 fZ = sh.z[p & (PR_ZRING - 1)][i][lane];
+            const float X[CPL] = {fX.x, fX.y, fX.z, fX.w};
+            const float yo[CPL] = {fYo.x, fYo.y, fYo.z, fYo.w};
+            const float zn[CPL] = {fZ.x, fZ.y, fZ.z, fZ.w};
+            const float mk[CPL] = {(float)(fMw & 0xFFu), (float)((fMw >> 8) & 0xFFu),
+                                   (float)((fMw >> 16) & 0xFFu), (float)(fMw >> 24)};
+            float Yv[CPL];
+#pragma unroll
+            for (int kk = 0; kk < CPL; ++kk) {
+                if (EXACT) {
+                    const float g = (-mk[kk] * (X[kk] - yo[kk])) / a.sigma2;
+                    Yv[kk] = lane_ok ? (X[kk] + a.c1 * g) + a.c2 * zn[kk] : 0.f;
+                } else {
+                    const float g = (mk[kk] * (yo[kk] - X[kk])) * a.inv_sigma2;
+                    Yv[kk] = lane_ok ? __builtin_fmaf(a.c2, zn[kk], __builtin_fmaf(a.c1, g, X[kk])) : 0.f;
+                }
+            }
+            // component-wise selects: a select of whole float4 objects becomes a select of their addresses
+            // (scratch memory)
+            oY[i] = make_float4(Yv[0], Yv[1], Yv[2], Yv[3]);
+            float xs[CPL];
+#pragma unroll
+            for (int kk = 0; kk < CPL; ++kk) xs[kk] = lane_ok ? (fresh ? Yv[kk] : X[kk]) : 0.f;
+            oX[i] = make_float4(xs[0], xs[1], xs[2], xs[3]);
+            const float uk = fresh ? 0.f : 1.f;     // (u2 of a fresh TV start is 0; the loaded values are finite)
+            oU0[i] = fresh ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(fU0.x, fU0.z, fU1.x, fU1.z);
+            oU1[i] = fresh ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(fU0.y, fU0.w, fU1.y, fU1.w);
+            (void)uk;
+        };
+        for (int t = T0; t < T1; ++t) {
+            const int phs = (t - f) & 3;
+            const int p = t + 4 - phs;
+            const bool live = p >= 0 && 2 * p < Q;
+            // ---- W-phase
+            if (phs == 0) {
+                if (t >= 0 && 2 * t < Q) {                   // hand pair t to stage 1
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        sh.x2[0][i][lane] = oX[i];
+                        sh.u0[0][i][lane] = oU0[i];
+                        sh.u1[0][i][lane] = oU1[i];
+                        sh.y[pr_yslot(2 * t + i)][lane] = oY[i];
+                    }
+                }
+                if (live) { dma(2 * p, 0, 3); dma(2 * p, 0, 4); dma(2 * p + 1, 1, 0); }
+            } else if (phs == 3 && live) {
+                wait_vm0();                                   // pair p's loads landed
+                data_term(p, 0);
+            }
+            lds_barrier();
+            // ---- C-phase
+            if (phs == 0) {
+                if (live) { dma(2 * p + 1, 1, 1); dma(2 * p + 1, 1, 2); dma(2 * p + 1, 1, 3); dma(2 * p + 1, 1, 4); }
+            } else if (phs == 3) {
+                if (live) data_term(p, 1);
+                // row a's staging was read in this step's W-phase (drained by the barrier)
+                if (p + 4 >= 0 && 2 * (p + 4) < Q) { dma(2 * p + 8, 0, 0); dma(2 * p + 8, 0, 1); dma(2 * p + 8, 0, 2); }
+            }
+            lds_barrier();
+        }
+    } else if (role == 1) {
+        // ---------------- STAGE k_st (one inner TV iteration per wave; stages 1..3 also the noise) ----------------
+        __builtin_amdgcn_s_setprio(1);
+        const int lastk = W - 1 - gj0;                     // in 0..3 on the lane holding column W-1
+        if (trk) pair_stage<EXACT, true>(a, sh, rm, k_st, T0, T1, lane, lastk, lane_ok, step);
+        else pair_stage<EXACT, false>(a, sh, rm, k_st, T0, T1, lane, lastk, lane_ok, step);
+    } else if (role == 3) {
+        for (int t = T0; t < T1; ++t) { lds_barrier(); lds_barrier(); }
+    } else {
+        // ---------------- BACK: steps t = bw (mod 2), rows (2t - 3n, 2t - 3n + 1) of ring n ----------------
+        // Per pair (4 half-steps): C_t ring n + staging reads, accumulators, X stores, mean / sq DMA of row a
+        // of the pair of step t + 4; W_{t+1} u2 stores; C_{t+1} its row b DMA, row a's accumulator / sample
+        // stores; W_{t+2} row b's.
+        const int bw = w - SP_FRONT - n;
+        __builtin_amdgcn_s_setprio(3);
+        const StepInfo si = step_info(a, step, a.mean[par_out]);
+        const float* mean_in = a.mean[par_in];
+        const float* sq_in = a.sq[par_in];
+        const bool need_prev = si.acc && !si.first;
+        const int Qb = qc1;                                 // rows past the core end are never stored
+        auto row0 = [&](int t) __attribute__((always_inline)) { return 2 * t - 3 * n; };
+        auto stored = [&](int q) __attribute__((always_inline)) { return q >= qc0 && q < Qb; };
+        int nvm = 0;                                        // vector-memory ops issued by this wave
+        int mark0 = 0, mark1 = 0;                           // nvm after the mean / sq DMA into buffer 0 / 1
+        auto dma_row = [&](int t, int i) __attribute__((always_inline)) {                  // mean / sq of row i of the pair of step t
+            const int bi = ((t - bw) >> 1) & 1;
+            const int q = row0(t) + i;
+            if (need_prev && stored(q)) {
+                int pl, rr;
+                locate(q, pl, rr);
+                const size_t base = (size_t)pl * HW + (size_t)rr * W + gjc;
+                glds16(mean_in + base, &sh.bst[bw][bi][i][0][0]);
+                glds16(sq_in + base, &sh.bst[bw][bi][i][1][0]);
+                nvm += 2;
+            }
+            if (i == 1) { if (bi) mark1 = nvm; else mark0 = nvm; }
+        };
+        const int tb0 = T0 + ((bw - T0) & 1);
+        dma_row(tb0, 0); dma_row(tb0, 1);
+        dma_row(tb0 + 2, 0); dma_row(tb0 + 2, 1);
+        const int nheld = ((si.acc && (si.blockend || si.liveout)) ? 2 : 0) + (si.sample ? 1 : 0);
+        bool ok[2] = {false, false};                        // the pair's rows that are stored
+        size_t hb[2] = {0, 0};
+        float4 hU0[2], hU1[2], hM[2], hQ[2], hX[2];
+        for (int i = 0; i < 2; ++i) hU0[i] = hU1[i] = hM[i] = hQ[i] = hX[i] = zero4;
+        auto held = [&](int i) __attribute__((always_inline)) {                            // accumulator / block-mean / sample stores of row i
+            if (!ok[i]) return;
+            if (lane_ok) {
+                if (si.acc) {
+                    if (si.blockend) {
+                        st_nt(a.blocks + (size_t)si.blk * BE + hb[i], hM[i]);
+                        st_nt(a.blocks2 + (size_t)si.blk * BE + hb[i], hQ[i]);
+                    } else if (si.liveout) {
+                        st_nt(a.mean[par_out] + hb[i], hM[i]);
+                        st_nt(a.sq[par_out] + hb[i], hQ[i]);
+                    }
+                }
+                if (si.sample) st_nt(a.samples + (size_t)si.sidx * BE + hb[i], hX[i]);
+            }
+            nvm += nheld;
+        };
+        for (int t = T0; t < T1; ++t) {
+            const bool mine = ((t - bw) & 1) == 0;          // C_t takes a pair
+            // ---- W-phase
+            if (!mine) {                                    // W_{t'+1} of the pair taken at t' = t - 1
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    if (!ok[i]) continue;
+                    if (lane_ok) {
+                        float* u2o = a.u2[par_out] + 2 * hb[i];
+                        st_nt(u2o, make_float4(hU0[i].x, hU1[i].x, hU0[i].y, hU1[i].y));
+                        st_nt(u2o + 4, make_float4(hU0[i].z, hU1[i].z, hU0[i].w, hU1[i].w));
+                    }
+                    nvm += 2;
+                }
+            } else {
+                held(1);                                    // W_{t'+2} of the pair taken at t' = t - 2
+                ok[1] = false;
+            }
+            lds_barrier();
+            // ---- C-phase
+            if (mine) {
+                const int c = row0(t);
+                const int bi = ((t - bw) >> 1) & 1;
+                ok[0] = stored(c);
+                ok[1] = stored(c + 1);
+                if (ok[0] || ok[1]) {
+                    if (si.acc && need_prev) wait_vm_n(nvm - (bi ? mark1 : mark0));   // this pair's mean / sq
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const float4 X2 = sh.x2[n][i][lane];
+                        hU0[i] = sh.u0[n][i][lane];
+                        hU1[i] = sh.u1[n][i][lane];
+                        hX[i] = X2;
+                        hM[i] = hQ[i] = zero4;
+                        if (si.acc) {
+                            float4 bm = zero4, bq = zero4;
+                            if (need_prev) {
+                                bm = sh.bst[bw][bi][i][0][lane];
+                                bq = sh.bst[bw][bi][i][1][lane];
+                            }
+                            const float xs[CPL] = {X2.x, X2.y, X2.z, X2.w};
+                            const float ms[CPL] = {bm.x, bm.y, bm.z, bm.w};
+                            const float qs[CPL] = {bq.x, bq.y, bq.z, bq.w};
+                            float m[CPL], qq[CPL];
+#pragma unroll
+                            for (int kk = 0; kk < CPL; ++kk) {
+                                if (si.first) {
+                                    m[kk] = si.cb * xs[kk];
+                                    qq[kk] = si.cb * (xs[kk] * xs[kk]);
+                                } else {
+                                    m[kk] = si.ca * ms[kk] + si.cb * xs[kk];
+                                    qq[kk] = si.ca * qs[kk] + si.cb * (xs[kk] * xs[kk]);
+                                }
+                            }
+                            hM[i] = make_float4(m[0], m[1], m[2], m[3]);
+                            hQ[i] = make_float4(qq[0], qq[1], qq[2], qq[3]);
+                        }
+                    }
+                    // every staging read returned before the buffer is re-targeted (pair of step t + 4)
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        if (!ok[i]) continue;
+                        int pl, rr;
+                        locate(c + i, pl, rr);
+                        hb[i] = (size_t)pl * HW + (size_t)rr * W + gj0;
+                        if (lane_ok) st_nt(a.x[par_out] + hb[i], hX[i]);
+                        nvm += 1;
+                    }
+                }
+                dma_row(t + 4, 0);
+            } else {                                        // C_{t'+1} of the pair taken at t' = t - 1
+                dma_row(t + 3, 1);
+                held(0);
+                ok[0] = false;
+            }
+            lds_barrier();
+        }
+    }
+}
+
+template <bool EXACT>
+__global__ void __launch_bounds__(TV_THREADS) tv_pair_kernel(const TvArgs a) {
+    __shared__ PairShared sh;
+    __shared__ int s_stop[MAXG];
+    __shared__ int s_flag, s_item, s_next;
+    const int C = a.C;
+    const long long step = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
+    const bool fresh = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
+    {
+        RowMap rm;
+        build_rowmap(a, blockIdx.x, rm);
+        pair_pass<EXACT>(a, sh, rm, a.n_tv, true, step, fresh);
+        if (!a.fin_inline) return;        // main-pass-only launch (kernel timing): no side effects
+        // rel_err partial sums of this stream -> global, per segment's chain (deepinv's early-stop
+        // test, per chain); the tracking stages wrote sh.red[segment][k - 1]
+        lds_barrier();
+        for (int tt = threadIdx.x; tt < SP_MAXSEG * SP_MAXST; tt += blockDim.x) {
+            const int sg = tt / SP_MAXST, it = tt - sg * SP_MAXST;     // it = k - 1
+            if (sg < rm.ns && it >= 2 && it <= a.n_tv - 2) {
+                const int g = a.per_chain_norm ? rm.pl(sg) / C : 0;
+                atomicAdd(&a.norms[((size_t)g * a.n_tv + it) * 2], (double)sh.red[sg][it][0]);
+                atomicAdd(&a.norms[((size_t)g * a.n_tv + it) * 2 + 1], (double)sh.red[sg][it][1]);
+            }
+        }
+    }
+    // ---- step finalisation by the last workgroup to arrive (as tv_stream_kernel) ----
+    wait_vm0();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const int old = __hip_atomic_fetch_add(a.arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_flag = (old == (int)gridDim.x - 1) ? 1 : 0;
+        if (s_flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    wait_vm0();
+    __syncthreads();
+    if (!s_flag) return;
+    const int G = a.B;
+    for (int g = threadIdx.x; g < G; g += blockDim.x) s_stop[g] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < G * SP_MAXST; i += blockDim.x) {
+        const int g = i / SP_MAXST, t = i - g * SP_MAXST;
+        if (t >= 2 && t <= a.n_tv - 2) {
+            const double nd = a.norms[((size_t)g * a.n_tv + t) * 2];
+            const double nn = a.norms[((size_t)g * a.n_tv + t) * 2 + 1];
+            const float rel = (float)sqrt(nd) / (float)sqrt(nn);
+            if (rel < a.tol) atomicOr(&s_stop[g], 1 << t);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) { s_next = 0; s_item = 0; }
+    __syncthreads();
+    for (int g = threadIdx.x; g < G; g += blockDim.x) {
+        const int m = s_stop[g];
+        s_stop[g] = m ? (__ffs(m) - 1) + 1 : a.n_tv;
+        if (m) s_item = 1;
+    }
+    __syncthreads();
+    if (s_item == 0) s_next = 1 << 30;        // common case: nothing to redo
+    // rare: re-stream every plane of a stopped chain with the stopped iteration count (the step's
+    // inputs are intact: ping-pong state)
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int items = a.B * C;
+            int it = min(s_next, items), found = -1;
+            for (; it < items; ++it)
+                if (s_stop[it / C] < a.n_tv) { found = it; break; }
+            s_item = found;
+            s_next = it + 1;
+        }
+        __syncthreads();
+        const int item = __builtin_amdgcn_readfirstlane(s_item);
+        if (item < 0) break;
+        RowMap rm;
+        plane_rowmap(a.H, item, rm);
+        const int nstop = __builtin_amdgcn_readfirstlane(s_stop[item / C]);
+        pair_pass<EXACT>(a, sh, rm, nstop, false, step, fresh);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.B * a.n_tv * 2; i += blockDim.x) a.norms[i] = 0.0;
+    if (threadIdx.x == 0) {
+        *a.arrive = 0;
+        if (a.fresh_dev) *a.fresh_dev = 0;
+        if (a.advance_step && a.d_step) *a.d_step = *a.d_step + 1;
     }
 }
 
@@ -1813,14 +1991,11 @@ struct TileShared {
     int s_flag, s_item, s_next;
 };
 
-// RES (persistent multi-step kernel, section 3.1d of DESIGN.md): resident = the core rows' chain state
-// (x2 == X, u2) is still in the caller's registers from the previous step and the core rows' mean / sq in
-// sh.mst, so only the halo rows' X / u2 (the neighbour bands' outputs) and y / mask are loaded; the new
-// mean / sq rows are also written back to sh.mst.  nrm: the rel-err sums of this step.
-template <bool EXACT, bool ALPHA1, int R, bool RES = false>
+template <bool EXACT, bool ALPHA1, int R>
 __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int plane, int band, int n_it,
-                                        bool track, long long step, bool fresh, float (&x2)[R][CPL],
-                                        float (&u0)[R][CPL], float (&u1)[R][CPL], bool resident, double* nrm) {
+                                        bool track, long long step, bool fresh) {
+    float x2[R][CPL], u0[R][CPL], u1[R][CPL];
+    double* const nrm = a.norms;
     const int lane = threadIdx.x & (WAVE - 1);
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int H = a.H, W = a.W, C = a.C, h = a.halo;
@@ -1843,8 +2018,6 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
     int gi[R];
     bool rv[R], core[R];
     // ---- 1. every load of the tile in flight: state and observation to registers, mean / sq by DMA
-    // (RES: the state loads land straight in the state registers -- x2 == X for alpha == 1 --, and the
-    // rows whose state is resident load nothing; no second copy of the state is held)
     float4 fX[R], fY[R], fU0[R], fU1[R], fXS[R];
     uint32_t fM[R];
 #pragma unroll
@@ -1856,30 +2029,17 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
         fM[r] = 0u;
         if (rv[r] && colok) {
             const size_t base = poff + (size_t)gi[r] * W + gj0;
-            if (RES) {
-                if (!(resident && core[r])) {
-                    const float4 v = ld4(a.x[par_in] + base);
-                    x2[r][0] = v.x; x2[r][1] = v.y; x2[r][2] = v.z; x2[r][3] = v.w;
-                    if (!fresh) {
-                        const float4 p = ld4(a.u2[par_in] + 2 * base);
-                        const float4 q = ld4(a.u2[par_in] + 2 * base + 4);
-                        u0[r][0] = p.x; u1[r][0] = p.y; u0[r][1] = p.z; u1[r][1] = p.w;
-                        u0[r][2] = q.x; u1[r][2] = q.y; u0[r][3] = q.z; u1[r][3] = q.w;
-                    }
-                }
-            } else {
-                fX[r] = ld4(a.x[par_in] + base);
-                if (!fresh) {
-                    fU0[r] = ld4(a.u2[par_in] + 2 * base);
-                    fU1[r] = ld4(a.u2[par_in] + 2 * base + 4);
-                    if (!ALPHA1) fXS[r] = ld4(a.x2[par_in] + base);
-                }
+            fX[r] = ld4(a.x[par_in] + base);
+            if (!fresh) {
+                fU0[r] = ld4(a.u2[par_in] + 2 * base);
+                fU1[r] = ld4(a.u2[par_in] + 2 * base + 4);
+                if (!ALPHA1) fXS[r] = ld4(a.x2[par_in] + base);
             }
             fY[r] = ld4(a.yobs + (size_t)b * a.y_cs + (size_t)c * HW + (size_t)gi[r] * W + gj0);
             fM[r] = *reinterpret_cast<const uint32_t*>(a.mask + (size_t)b * a.m_cs + (size_t)gi[r] * W + gj0);
         }
     }
-    if (need_prev && n_it >= 0 && !(RES && resident)) {
+    if (need_prev && n_it >= 0) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             if (rv[r] && core[r]) {
@@ -1900,16 +2060,13 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const bool ok = rv[r] && colok;
-        const float X[CPL] = {RES ? x2[r][0] : fX[r].x, RES ? x2[r][1] : fX[r].y, RES ? x2[r][2] : fX[r].z,
-                              RES ? x2[r][3] : fX[r].w};
+        const float X[CPL] = {fX[r].x, fX[r].y, fX[r].z, fX[r].w};
         const float yo[CPL] = {fY[r].x, fY[r].y, fY[r].z, fY[r].w};
         const float mk[CPL] = {(float)(fM[r] & 0xFFu), (float)((fM[r] >> 8) & 0xFFu), (float)((fM[r] >> 16) & 0xFFu),
                                (float)(fM[r] >> 24)};
         const float xs[CPL] = {fXS[r].x, fXS[r].y, fXS[r].z, fXS[r].w};
-        const float us0[CPL] = {RES ? u0[r][0] : fU0[r].x, RES ? u0[r][1] : fU0[r].z, RES ? u0[r][2] : fU1[r].x,
-                                RES ? u0[r][3] : fU1[r].z};
-        const float us1[CPL] = {RES ? u1[r][0] : fU0[r].y, RES ? u1[r][1] : fU0[r].w, RES ? u1[r][2] : fU1[r].y,
-                                RES ? u1[r][3] : fU1[r].w};
+        const float us0[CPL] = {fU0[r].x, fU0[r].z, fU1[r].x, fU1[r].z};
+        const float us1[CPL] = {fU0[r].y, fU0[r].w, fU1[r].y, fU1[r].w};
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
             float Y;
@@ -1936,15 +2093,8 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
     // for the dual and one row more below for the primal (the dual of a row reads the next row's z);
     // a wave none of whose rows is needed skips the phase (its stale rows feed only unneeded rows).
     const int wr0 = e0 + w * R, wr1 = wr0 + R;
-#ifdef PSGLA_ABL_TILE_NOITER
-    n_it = 0;            // diagnostic timing build only: loads, noise, data term and stores
-#endif
     for (int it = 0; it < n_it; ++it) {
-#ifdef PSGLA_ABL_TILE_NOTRK
-        const bool trk = false;   // diagnostic timing build only
-#else
         const bool trk = track && it >= trk_lo(a) && it <= trk_hi(a);
-#endif
         float sd = 0.f, sn = 0.f;
         const int span = n_it - 1 - it;
         const bool act_p = wr1 > r0 - span && wr0 < r1 + span + 1;
@@ -1998,9 +2148,7 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
             const float2 rs = row_sum2(colok ? sd : 0.f, colok ? sn : 0.f);
             if ((lane & 15) == 0) sh.red[it][w][lane >> 4] = rs;
         }
-#ifndef PSGLA_ABL_TILE_NOBAR
         __syncthreads();
-#endif
         // dual: u = prox_sigma_g_conj(u2 + sigma nabla z, ths); u2 += rho (u - u2)
         const float4 dn = (w < TV_NW - 1) ? sh.zrow[w + 1][lane] : zero4;
 #pragma unroll
@@ -2036,9 +2184,7 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
             }
         }
         if (act_d) sh.urow[w][lane] = make_float4(u0[R - 1][0], u0[R - 1][1], u0[R - 1][2], u0[R - 1][3]);
-#ifndef PSGLA_ABL_TILE_NOBAR
         __syncthreads();
-#endif
     }
     // ---- 5. rel_err partial sums -> the chain's norms (one fp64 atomic per iteration and workgroup)
     if (track) {
@@ -2089,11 +2235,6 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
             }
             const float4 M4 = make_float4(m[0], m[1], m[2], m[3]);
             const float4 Q4 = make_float4(q[0], q[1], q[2], q[3]);
-            if (RES) {
-                // the next step's running mean / sq of this row (the wave's own LDS rows)
-                sh.mst[w * R + r][0][lane] = M4;
-                sh.mst[w * R + r][1][lane] = Q4;
-            }
             if (si.blockend) {
                 st_tile(a.blocks + (size_t)si.blk * BE + base, M4);
                 st_tile(a.blocks2 + (size_t)si.blk * BE + base, Q4);
@@ -2118,23 +2259,13 @@ __global__ void __launch_bounds__(TV_THREADS) tv_tile_kernel(const TvArgs a) {
         const int x = blockIdx.x, xcd = x & 7, k = x >> 3;
         const int plane = (k / T) * 8 + xcd;
         const int band = k - (k / T) * T;
-        float x2[R][CPL], u0[R][CPL], u1[R][CPL];
-        if (plane < P) sb_tile<EXACT, ALPHA1, R>(a, sh, plane, band, a.n_tv, true, step, fresh, x2, u0, u1, false, a.norms);
+        if (plane < P) sb_tile<EXACT, ALPHA1, R>(a, sh, plane, band, a.n_tv, true, step, fresh);
     }
-#ifdef PSGLA_ABL_TILE_NOFIN
-    return;              // diagnostic timing build only: no arrival / finalisation
-#endif
     if (!a.fin_inline) return;
     // ---- step finalisation by the last workgroup to arrive (as tv_stream_kernel) ----
-#ifndef PSGLA_ABL_TILE_NOWAIT
     wait_vm0();
-#endif
     __syncthreads();
     if (threadIdx.x == 0) {
-#ifdef PSGLA_TILE_FENCED
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
         // Without fences: every output of this kernel is an sc1 (write-through) store and every rel-err sum
         // an agent-scope atomic; each wave waited vmcnt(0) before the barrier above, one lane per workgroup
         // adds to the arrival counter, and the workgroup whose add returns the last count reads the sums by
@@ -2143,17 +2274,10 @@ __global__ void __launch_bounds__(TV_THREADS) tv_tile_kernel(const TvArgs a) {
         // (the rare redo reads the step's inputs, written by the previous launch).
         const int old = __hip_atomic_fetch_add(a.arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sh.s_flag = (old == (int)gridDim.x - 1) ? 1 : 0;
-#ifdef PSGLA_TILE_FENCED
-        if (sh.s_flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
     }
     wait_vm0();
     __syncthreads();
     if (!sh.s_flag) return;
-#ifdef PSGLA_ABL_TILE_NOLAST
-    if (threadIdx.x == 0) { *a.arrive = 0; if (a.advance_step && a.d_step) *a.d_step = step - a.step_offset + 1; }
-    return;              // diagnostic timing build only
-#endif
     const int G = a.B;
     for (int g = threadIdx.x; g < G; g += blockDim.x) sh.s_stop[g] = 0;
     __syncthreads();
@@ -2185,681 +2309,11 @@ __global__ void __launch_bounds__(TV_THREADS) tv_tile_kernel(const TvArgs a) {
             const int plane = item / T, band = item - plane * T;
             const int nstop = __builtin_amdgcn_readfirstlane(sh.s_stop[plane / a.C]);
             if (nstop < a.n_tv) {
-                float x2[R][CPL], u0[R][CPL], u1[R][CPL];
-                sb_tile<EXACT, ALPHA1, R>(a, sh, plane, band, nstop, false, step, fresh, x2, u0, u1, false, a.norms);
+                sb_tile<EXACT, ALPHA1, R>(a, sh, plane, band, nstop, false, step, fresh);
                 wait_vm0();
                 __syncthreads();
             }
         }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < a.B * a.n_tv * 2; i += blockDim.x) a.norms[i] = 0.0;
-    if (threadIdx.x == 0) {
-        *a.arrive = 0;
-        if (a.fresh_dev) *a.fresh_dev = 0;
-        if (a.advance_step && a.d_step) *a.d_step = step - a.step_offset + 1;   // the value read at the start: no dependent load
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-// Persistent multi-step tile kernel (alpha == 1, all tiles co-resident).
-//
-// One launch runs a.msteps consecutive Langevin steps of the tile kernel.  A tile's core rows keep
-// their chain state (X == x2, u2) in registers and their running mean / sq in LDS from one step to
-// the next, so a step loads only the halo rows' X / u2 (the neighbour bands' outputs of the previous
-// step) and y / mask; outputs are still stored every step (they are the halo of the neighbours and
-// the inputs of the rare early-stop redo).  Steps are separated by a grid barrier (every workgroup is
-// resident: the host launches this kernel only when grid <= CUs); after it EVERY workgroup reads all
-// chains' rel-err sums of the step and takes deepinv's early-stop decision itself, so no workgroup
-// waits for a last one to finalise.  A chain that stopped is recomputed by its own tiles from the
-// step's inputs (double-buffered, intact) and a second grid barrier publishes the redone rows.
-// The rel-err sums rotate over three buffers by step % 3: workgroup 0 clears the one of step s + 1
-// during step s (everyone finished reading it before arriving at barrier s - 1).  Barrier waits are
-// bounded (a.arrive[3] = 1 reports a timeout; the results of such a launch are invalid).
-// ---------------------------------------------------------------------------------------
-constexpr int GS_SPIN_MAX = 1 << 22;
-
-__device__ __forceinline__ double* step_norms(const TvArgs& a, long long step) {
-    const int m = (int)(((step % 3) + 3) % 3);
-    return m == 0 ? a.norms : a.norms_ring + (size_t)(m - 1) * a.B * a.n_tv * 2;
-}
-
-// Grid-wide barrier on counter gs[1] (monotonic within a launch): every wave has waited for its own
-// stores / atomics, then ONE wave per workgroup releases, waits (bounded) and acquires (the acquire
-// invalidates the CU's L1 and the XCD's L2 lines for the whole workgroup; an acquire by every wave
-// made the step 2.5x slower) before the workgroup barrier lets the other waves load.
-__device__ __forceinline__ void grid_sync(int* gs, int target) {
-    wait_vm0();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-#ifndef PSGLA_MS_NOREL
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#endif
-#ifdef PSGLA_MS_FLAG
-        // the last arriver publishes the barrier generation in gs[0]; the others poll that word (no
-        // polling loads on the line the arrival atomics serialise on)
-        const int old = __hip_atomic_fetch_add(&gs[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == target - 1) __hip_atomic_store(&gs[0], target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int* const pw = &gs[0];
-#else
-        __hip_atomic_fetch_add(&gs[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int* const pw = &gs[1];
-#endif
-        int spins = 0;
-        while (__hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > GS_SPIN_MAX) {
-                __hip_atomic_fetch_or(&gs[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-#ifdef PSGLA_MS_L1INV
-        asm volatile("buffer_inv sc0\n\ts_waitcnt vmcnt(0)" ::: "memory");
-#else
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
-        wait_vm0();
-    }
-    __syncthreads();
-}
-
-template <bool EXACT, int R>
-__global__ void __launch_bounds__(TV_THREADS) tv_tile_multi_kernel(const TvArgs a) {
-    __shared__ TileShared<R> sh;
-    const long long step0 = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
-    const bool fresh0 = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
-    const int P = a.B * a.C;
-    const int T = a.nbands;
-    const int x = blockIdx.x, xcd = x & 7, k = x >> 3;
-    const int plane = (k / T) * 8 + xcd;            // all bands of a plane on one XCD (as tv_tile_kernel)
-    const int band = k - (k / T) * T;
-    const bool act = plane < P;
-    const int G = a.B;
-    const int NG = (int)gridDim.x;
-    const size_t nb = (size_t)a.B * a.n_tv * 2;
-    int* const gs = a.arrive;                       // [1] barrier count, [2] exit count, [3] timeout flag
-    float x2[R][CPL], u0[R][CPL], u1[R][CPL];       // the core rows' state, resident across steps
-    int target = 0;
-    for (int i = 0; i < a.msteps; ++i) {
-        const long long step = step0 + i;
-        const bool fresh = fresh0 && i == 0;
-        double* const nrm = step_norms(a, step);
-        if (act) sb_tile<EXACT, true, R, true>(a, sh, plane, band, a.n_tv, true, step, fresh, x2, u0, u1, i > 0, nrm);
-        if (blockIdx.x == 0) {
-            double* const nx = step_norms(a, step + 1);
-            for (size_t j = threadIdx.x; j < nb; j += blockDim.x)
-                __hip_atomic_store(&nx[j], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        target += NG;
-        grid_sync(gs, target);
-#ifdef PSGLA_MS_NODECIDE
-        continue;            // diagnostic timing build only: no early-stop decision
-#endif
-        // deepinv's early stop of every chain, decided by every workgroup from the step's sums
-        for (int g = threadIdx.x; g < G; g += blockDim.x) sh.s_stop[g] = 0;
-        if (threadIdx.x == 0) sh.s_item = 0;
-        __syncthreads();
-        for (int j = threadIdx.x; j < G * MAXIT; j += blockDim.x) {
-            const int g = j / MAXIT, t = j - g * MAXIT;
-            if (t >= trk_lo(a) && t <= trk_hi(a) && t < a.n_tv) {
-                const double nd = __hip_atomic_load(&nrm[((size_t)g * a.n_tv + t) * 2], __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-                const double nn = __hip_atomic_load(&nrm[((size_t)g * a.n_tv + t) * 2 + 1], __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-                const float rel = (float)sqrt(nd) / (float)sqrt(nn);
-                if (rel < a.tol) atomicOr(&sh.s_stop[g], 1 << t);
-            }
-        }
-        __syncthreads();
-        for (int g = threadIdx.x; g < G; g += blockDim.x) {
-            const int m = sh.s_stop[g];
-            sh.s_stop[g] = m ? (__ffs(m) - 1) + 1 : a.n_tv;
-            if (m) sh.s_item = 1;
-        }
-        __syncthreads();
-        if (sh.s_item) {
-            // rare: the tiles of a stopped chain are recomputed from the step's inputs with the stopped count
-            const int nstop = act ? sh.s_stop[plane / a.C] : a.n_tv;
-            if (act && nstop < a.n_tv)
-                sb_tile<EXACT, true, R, true>(a, sh, plane, band, nstop, false, step, fresh, x2, u0, u1, false, nrm);
-            target += NG;
-            grid_sync(gs, target);
-        }
-    }
-    // ---- exit: the last workgroup out clears the counters and every rel-err buffer, advances the step
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int old = __hip_atomic_fetch_add(&gs[2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sh.s_flag = (old == NG - 1) ? 1 : 0;
-    }
-    __syncthreads();
-    if (!sh.s_flag) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    for (size_t j = threadIdx.x; j < nb; j += blockDim.x) {
-        a.norms[j] = 0.0;
-        a.norms_ring[j] = 0.0;
-        a.norms_ring[nb + j] = 0.0;
-    }
-    if (threadIdx.x == 0) {
-        gs[0] = 0;
-        gs[1] = 0;
-        gs[2] = 0;
-        if (a.fresh_dev) *a.fresh_dev = 0;
-        if (a.advance_step && a.d_step) *a.d_step = step0 - a.step_offset + a.msteps;
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-// Per-wave pipelines: the fused step with no LDS ring and no barrier ("wave kernel",
-// kernel_variant 5).
-//
-// The stream kernel hands every row from one inner TV iteration (a wave) to the next through LDS
-// rings, one workgroup barrier per row (~34 ds_write_b128 + ~50 ds_read_b128 per row, 16 waves
-// released in lock-step): latency-bound at ~0.41 of the HBM roofline.  Here ONE wave runs the whole
-// pipeline of its own row range -- front (LDS-DMA loads, noise, data term), all n inner iterations,
-// back (relaxation, accumulators, stores) -- skewed by one row per iteration: at step t iteration k
-// runs its primal on stream row t - k + 1 and its dual on row t - k, so each input is either this
-// step's output of iteration k - 1 or the iteration's own state from the previous step.  That state
-// (u2^{k-1} and z^k of one row, x2^k of the same row: 16 VGPRs per iteration and lane) stays in
-// registers; LDS holds only the wave's own Y rows (prox anchor of rows t - n .. t) and its LDS-DMA
-// staging.  Nothing crosses waves.  8 waves per CU (2 per SIMD, <= 256 VGPRs) run independent
-// contiguous row ranges of the concatenated planes (build_rowmap), n halo rows where a range is cut
-// inside a plane; iteration k computes only the rows the core's dependency cone needs (trapezoid).
-// The per-element arithmetic is the stream kernel's in both modes.  W <= 256, W % 4 == 0, ldw == W.
-// ---------------------------------------------------------------------------------------
-constexpr int WV_NW = 8;                  // waves (= row ranges) per workgroup
-constexpr int WV_THREADS = WV_NW * WAVE;
-constexpr int WV_YS = SP_MAXST + 1;       // Y ring slots: stream rows t - n .. t
-constexpr int WV_MAXC = 8;                // chains per workgroup whose rel-err sums meet in LDS first
-
-struct WaveLds {
-    float4 y[WV_YS][WAVE];                // Y rows by stream row % WV_YS
-    float4 fx[WAVE], fy[WAVE], fu0[WAVE], fu1[WAVE], fxs[WAVE];   // front staging: X, y, u2, x2
-    uint32_t fm[WAVE];                    // front staging: mask (4 columns per lane)
-    float4 bm[WAVE], bq[WAVE];            // back staging: mean / sq of the back's row
-    float red[SP_MAXSEG][SP_MAXST][2];    // rel-err partial sums per (segment, inner iteration)
-};
-struct WaveShared {
-    WaveLds w[WV_NW];
-    int s_stop[MAXG];
-    double wred[WV_MAXC][SP_MAXST][2];
-    int s_flag, s_item;
-};
-
-// Primal update of one row (deepinv: x = prox_tau_fx(x2 - tau nabla^T u2, Y); z = 2x - x2;
-// x2 += rho (x - x2)), the stream kernel's stage_phase_a arithmetic.  dx: (x - x2_prev) in fast mode
-// (the rel-err term), unused in exact mode.
-template <bool EXACT>
-__device__ __forceinline__ void wv_primal(const TvArgs& a, const float (&xo)[CPL], const float (&u0)[CPL],
-                                          const float (&u1)[CPL], const float (&yy)[CPL], const float (&pu0)[CPL],
-                                          float (&z)[CPL], float (&xn)[CPL], float (&dx)[CPL]) {
-    // u1 of the column left of this lane's first column (lane-1's last); 0 at lane 0
-    const float u1l = __int_as_float(
-        __builtin_amdgcn_update_dpp(0, __float_as_int(u1[CPL - 1]), 0x138 /* wave_shr:1 */, 0xF, 0xF, true));
-#pragma unroll
-    for (int kk = 0; kk < CPL; ++kk) {
-        const float u1left = kk > 0 ? u1[kk - 1] : u1l;
-        const float tt = ((pu0[kk] - u0[kk]) - u1[kk]) + u1left;
-        const float x = xo[kk];
-        if (EXACT) {
-            const float xv = ((x - a.tau * tt) + a.tau * yy[kk]) / a.opt;
-            z[kk] = 2.0f * xv - x;
-            xn[kk] = x + a.rho * (xv - x);
-            dx[kk] = 0.f;
-        } else {
-            const float xv = __builtin_fmaf(a.tau, yy[kk] - tt, x) * a.inv_opt;
-            z[kk] = __builtin_fmaf(2.0f, xv, -x);
-            dx[kk] = xv - x;
-            xn[kk] = __builtin_fmaf(a.rho, dx[kk], x);
-        }
-    }
-}
-
-// Dual update of one row (deepinv: u = prox_sigma_g_conj(u2 + sigma nabla z, ths); u2 += rho (u - u2)),
-// the stream kernel's stage_phase_b arithmetic.  DN: the row has a row below (zd = its z).
-template <bool EXACT, bool DN>
-__device__ __forceinline__ void wv_dual(const TvArgs& a, const float (&u0)[CPL], const float (&u1)[CPL],
-                                        const float (&zc)[CPL], const float (&zd)[CPL], bool lastlane,
-                                        float (&un0)[CPL], float (&un1)[CPL]) {
-    // z of the column right of this lane's last column (lane+1's first)
-    const float zr3 = __int_as_float(
-        __builtin_amdgcn_update_dpp(0, __float_as_int(zc[0]), 0x130 /* wave_shl:1 */, 0xF, 0xF, true));
-#pragma unroll
-    for (int kk = 0; kk < CPL; ++kk) {
-        const float z = zc[kk];
-        const float zr = kk < CPL - 1 ? zc[kk + 1] : zr3;
-        const float g0 = DN ? (zd[kk] - z) : 0.0f;
-        float g1 = zr - z;
-        if (kk == CPL - 1) g1 = lastlane ? 0.0f : g1;     // the image's last column (W % 4 == 0)
-        const float uo0 = u0[kk], uo1 = u1[kk];
-        if (EXACT) {
-            const float v0 = uo0 + a.sig_tv * g0;
-            const float v1 = uo1 + a.sig_tv * g1;
-            const float nrm = sqrtf(v0 * v0 + v1 * v1) / a.ths;
-            const float dd = fmaxf(nrm, 1.0f);
-            un0[kk] = uo0 + a.rho * (v0 / dd - uo0);
-            un1[kk] = uo1 + a.rho * (v1 / dd - uo1);
-        } else {
-            const float v0 = __builtin_fmaf(a.sig_tv, g0, uo0);
-            const float v1 = __builtin_fmaf(a.sig_tv, g1, uo1);
-            const float s2 = __builtin_fmaf(v0, v0, v1 * v1);
-            const float f = fminf(1.0f, a.ths * __builtin_amdgcn_rsqf(s2));
-            un0[kk] = __builtin_fmaf(a.rho, __builtin_fmaf(v0, f, -uo0), uo0);
-            un1[kk] = __builtin_fmaf(a.rho, __builtin_fmaf(v1, f, -uo1), uo1);
-        }
-    }
-}
-
-// Row range of one wave: core rows [H part / parts, H (part + 1) / parts) of `plane` and the h halo rows
-// around them inside the plane (a RowMap with one segment; ranges never cross a plane boundary).
-// Q = 0: empty part.
-__device__ __forceinline__ void part_rowmap(int H, int h, int plane, int part, int parts, RowMap& m) {
-    const int c0 = H * part / parts, c1 = H * (part + 1) / parts;
-    const int lo = max(0, c0 - h), hi = min(H, c1 + h);
-    m.ns = 1;
-    m.Q = c1 > c0 ? hi - lo : 0;
-    m.htop = c0 - lo;
-    m.hbot = hi - c1;
-    m.q1 = m.q2 = m.q3 = m.Q;
-    m.pl0 = plane; m.pl1 = m.pl2 = m.pl3 = 0;
-    m.lo0 = lo; m.lo1 = m.lo2 = m.lo3 = 0;
-}
-
-// Range slot g of a launch -> its plane and part.  wv_whole == 0: plane p is cut into wv_base parts
-// (wv_base + 1 for the first wv_extra planes), one per slot; wv_whole == 1 (more planes than slots):
-// slot g takes the whole planes g, g + slots, ... (item i of the slot).  false: nothing (more).
-__device__ __forceinline__ bool wave_item(const TvArgs& a, int g, int i, int& plane, int& part, int& parts) {
-    const int P = a.B * a.C;
-    if (a.wv_whole) {
-        plane = g + i * a.wv_slots;
-        part = 0;
-        parts = 1;
-        return plane < P;
-    }
-    if (i > 0) return false;
-    const int big = a.wv_base + 1, nbig = a.wv_extra * big;
-    if (g < nbig) {
-        plane = g / big; part = g - plane * big; parts = big;
-    } else {
-        const int g2 = g - nbig;
-        plane = a.wv_extra + g2 / a.wv_base; part = g2 - (plane - a.wv_extra) * a.wv_base; parts = a.wv_base;
-    }
-    return plane < P;
-}
-
-template <int M> struct WvMode { static constexpr int v = M; };
-
-// One wave's pass over the rows of `rm` (one plane, rows lo0 .. lo0 + Q - 1) with n inner iterations.
-// track: deepinv's rel-err terms of the core rows are added to the chain's sums (the workgroup's LDS
-// accumulator wred for chains c0g .. c0g + WV_MAXC - 1, else the global ones).
-//
-// Schedule: at step t the front loads / makes row t; iteration k runs its primal on row p = t - k + 1
-// (inputs x2^{k-1}, u2^{k-1} of row p handed on from iteration k - 1 within the step, the row above's
-// u2^{k-1}[..., 0] from its own state) and its dual on row p - 1 (its own state: u2^{k-1}, z^k of row
-// p - 1, and the new z of row p); the back finishes row t - n.  Iteration k runs the rows
-// [max(0, lo_k - 1), hi_k] with lo_k = max(0, qc0 - (n - k)), hi_k = min(Q, qc1 + n - k) (the core's
-// dependency cone, one row more at each end); where the stream ends at the plane's bottom the row
-// p = Q is a virtual primal (z of row Q := z of row Q - 1, so the dual of the last row sees no vertical
-// difference, as deepinv's nabla).  The state starts at zero, so the first primal of a plane-top stream
-// sees u2 = 0 above, as deepinv's nabla^T.
-template <bool EXACT, bool ALPHA1>
-__device__ __forceinline__ void wave_pass(const TvArgs& a, WaveLds& L, const RowMap& rm, const int n,
-                                          const bool track, const long long step, const bool fresh,
-                                          double (*wred)[SP_MAXST][2], const int c0g) {
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int H = a.H, W = a.W, C = a.C;
-    const size_t HW = (size_t)H * W;
-    const size_t E = (size_t)C * HW;
-    const size_t BE = (size_t)a.B * E;
-    const int par_in = (int)(step & 1), par_out = (int)((step + 1) & 1);
-    const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int Q = rm.Q;
-    const int qc0 = rm.htop, qc1 = Q - rm.hbot;          // core stream rows
-    const bool bottom = rm.hbot == 0;                     // the stream ends at the plane's last row
-    const int plane = rm.pl0, r0 = rm.lo0;                // stream row q = plane row r0 + q
-    const int chain = plane / C, cc = plane - chain * C;
-    const int gj0 = CPL * lane;
-    const bool lane_ok = gj0 < W;
-    const int gjc = min(gj0, W - CPL);                     // DMA source column (every lane in bounds)
-    const bool lastlane = gj0 + CPL == W;
-    const StepInfo si = step_info(a, step, a.mean[par_out]);
-    const bool need_prev = si.acc && !si.first;
-    const size_t pbase = (size_t)plane * HW + (size_t)r0 * W;          // stream row 0 of the state buffers
-    const size_t ybase = (size_t)chain * a.y_cs + (size_t)cc * HW + (size_t)r0 * W;
-    const size_t mbase = (size_t)chain * a.m_cs + (size_t)r0 * W;
-    const uint32_t vo_c = (uint32_t)gjc * 4u;              // byte offsets in a row: DMA lanes (clamped) / stores
-    const uint32_t vo_s = (uint32_t)gj0 * 4u;
-    // vector-memory stores per core row of the back (lane 0 always holds a real column: every store issues)
-    const int nst = 3 + (ALPHA1 ? 0 : 1) + ((si.acc && (si.blockend || si.liveout)) ? 2 : 0) + (si.sample ? 1 : 0);
-
-    auto lo_k = [&](int k) { return max(0, qc0 - (n - k)); };
-    auto hi_k = [&](int k) { return min(Q, qc1 + (n - k)); };
-    // iteration k runs its primal at steps [tb_k, te_k] (rows max(0, lo_k - 1) .. hi_k, and the virtual
-    // row Q below a plane-bottom stream); tb_k and te_k do not decrease with k, so the iterations active
-    // at a step are an interval [kmin, kmax]
-    auto tb_k = [&](int k) { return max(0, lo_k(k) - 1) + k - 1; };
-    auto te_k = [&](int k) { return (bottom ? hi_k(k) : min(hi_k(k), Q - 1)) + k - 1; };
-    const int t_beg = max(0, lo_k(1) - 1);                // front rows [t_beg, t_fend)
-    const int t_fend = min(Q, hi_k(1) + 1);
-    const int nsteps = qc1 + n;                            // the back finishes core row qc1 - 1
-    // steady steps (n == SP_MAXST only): every iteration on a real row, front active: [t_st0, t_st1)
-    const int t_st0 = n == SP_MAXST ? max(t_beg, tb_k(n)) : nsteps;
-    const int t_st1 = n == SP_MAXST ? min(t_fend, min(nsteps, min(Q, hi_k(n) + 1) + n - 1)) : nsteps;
-    // bases of this stream's row 0 (accumulators: the live means or the block slot; the sample slot)
-    float* const xo_g = a.x[par_out] + pbase;
-    float* const u2o_g = a.u2[par_out] + 2 * pbase;
-    float* const x2o_g = ALPHA1 ? nullptr : a.x2[par_out] + pbase;
-    float* const accm_g = !si.acc ? nullptr : (si.blockend ? a.blocks + (size_t)si.blk * BE + pbase : (si.liveout ? a.mean[par_out] + pbase : nullptr));
-    float* const accq_g = !si.acc ? nullptr : (si.blockend ? a.blocks2 + (size_t)si.blk * BE + pbase : (si.liveout ? a.sq[par_out] + pbase : nullptr));
-    float* const smp_g = si.sample ? a.samples + (size_t)si.sidx * BE + pbase : nullptr;
-    const float* const xi_g = a.x[par_in] + pbase;
-    const float* const u2i_g = a.u2[par_in] + 2 * pbase;
-    const float* const x2i_g = ALPHA1 ? nullptr : a.x2[par_in] + pbase;
-    const float* const yi_g = a.yobs + ybase;
-    const uint8_t* const mi_g = a.mask + mbase;
-    const float* const mean_in = a.mean[par_in] + pbase;
-    const float* const sq_in = a.sq[par_in] + pbase;
-
-    auto front_dma = [&](int q) {
-        const size_t o = (size_t)q * W;
-        sglds16(xi_g + o, vo_c, &L.fx[0]);
-        sglds16(yi_g + o, vo_c, &L.fy[0]);
-        sglds16(u2i_g + 2 * o, 2u * vo_c, &L.fu0[0]);
-        sglds16(u2i_g + 2 * o + 4, 2u * vo_c, &L.fu1[0]);
-        sglds4(mi_g + o, (uint32_t)gjc, &L.fm[0]);
-        if (!ALPHA1) sglds16(x2i_g + o, vo_c, &L.fxs[0]);
-    };
-    auto back_dma = [&](int q) {
-        const size_t o = (size_t)q * W;
-        sglds16(mean_in + o, vo_c, &L.bm[0]);
-        sglds16(sq_in + o, vo_c, &L.bq[0]);
-    };
-
-    // iteration k's state (index k - 1): u2^{k-1} and z^k of the row of its last primal, x2^k of it
-    float Su0[SP_MAXST][CPL], Su1[SP_MAXST][CPL], Sz[SP_MAXST][CPL], Sx[SP_MAXST][CPL];
-#pragma unroll
-    for (int k = 0; k < SP_MAXST; ++k) {
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) { Su0[k][c] = 0.f; Su1[k][c] = 0.f; Sz[k][c] = 0.f; Sx[k][c] = 0.f; }
-    }
-    // rel-err sums: only iterations it = k - 1 in [2, n - 2] are tracked, i.e. k in [3, 9] (index k - 3)
-    constexpr int NTRK = SP_MAXST - 3;
-    float tsd[NTRK], tsn[NTRK];
-#pragma unroll
-    for (int i = 0; i < NTRK; ++i) { tsd[i] = 0.f; tsn[i] = 0.f; }
-
-    int nyoung = 0;                          // vector-memory ops issued after the front DMA of the next row
-    // one step: MODE 0 = steady (every iteration on a real row, front active), 1 = general (fill / drain)
-    auto do_step = [&](const int t, auto mode) {
-        constexpr int MODE = decltype(mode)::v;
-        int kmin = 1, kmax = SP_MAXST;
-        if (MODE == 1) {
-            kmin = n + 1;
-            kmax = 0;
-            for (int k = n; k >= 1; --k) {
-                if (te_k(k) >= t) kmin = k;
-                if (kmax == 0 && tb_k(k) <= t) kmax = k;
-            }
-        }
-        const int bq_row = t - n;            // the back's row
-        const bool bk = bq_row >= qc0 && bq_row < qc1;
-        // ---------------- front: row t -> Y(t), x2^0(t), u2^0(t) ----------------
-        float xin[CPL], ui0[CPL], ui1[CPL], yin[CPL];
-        if (MODE == 0 || t < t_fend) {
-            const size_t e = ((size_t)cc * H + (r0 + t)) * W + gj0;  // element index in the chain's C*H*W image
-            float Zn[CPL];
-            normal_quad(a.seed, (uint32_t)(a.chain0 + chain), (uint32_t)step, TAG_LANGEVIN, (uint32_t)(e >> 2), Zn);
-            wait_vm_n(nyoung);               // row t's staging landed (issued one step ago)
-            const float4 fX = L.fx[lane], fYo = L.fy[lane], fU0 = L.fu0[lane], fU1 = L.fu1[lane];
-            const float4 fXS = ALPHA1 ? zero4 : L.fxs[lane];
-            const uint32_t fM = L.fm[lane];
-            const float X[CPL] = {fX.x, fX.y, fX.z, fX.w};
-            const float yo[CPL] = {fYo.x, fYo.y, fYo.z, fYo.w};
-            const float mk[CPL] = {(float)(fM & 0xFFu), (float)((fM >> 8) & 0xFFu), (float)((fM >> 16) & 0xFFu),
-                                   (float)(fM >> 24)};
-            const float xs[CPL] = {fXS.x, fXS.y, fXS.z, fXS.w};
-            const float us0[CPL] = {fU0.x, fU0.z, fU1.x, fU1.z};
-            const float us1[CPL] = {fU0.y, fU0.w, fU1.y, fU1.w};
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                float Y;
-                if (EXACT) {
-                    const float g = (-mk[c] * (X[c] - yo[c])) / a.sigma2;
-                    Y = (X[c] + a.c1 * g) + a.c2 * Zn[c];
-                } else {
-                    const float g = (mk[c] * (yo[c] - X[c])) * a.inv_sigma2;
-                    Y = __builtin_fmaf(a.c2, Zn[c], __builtin_fmaf(a.c1, g, X[c]));
-                }
-                yin[c] = lane_ok ? Y : 0.f;
-                xin[c] = lane_ok ? (fresh ? Y : (ALPHA1 ? X[c] : xs[c])) : 0.f;
-                ui0[c] = (lane_ok && !fresh) ? us0[c] : 0.f;
-                ui1[c] = (lane_ok && !fresh) ? us1[c] : 0.f;
-            }
-            L.y[t % WV_YS][lane] = make_float4(yin[0], yin[1], yin[2], yin[3]);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // staging read before it is re-targeted
-            nyoung = 0;
-            if (t + 1 < t_fend) front_dma(t + 1);
-            if (bk && need_prev) { back_dma(bq_row); nyoung = 2; }
-        } else {
-            if (bk && need_prev) back_dma(bq_row);
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) { xin[c] = 0.f; ui0[c] = 0.f; ui1[c] = 0.f; yin[c] = 0.f; }
-        }
-        // ---------------- inner iterations k = 1..n ----------------
-#pragma unroll
-        for (int k = 1; k <= SP_MAXST; ++k) {
-            const int p = t - k + 1;
-            if (MODE == 0 || (k >= kmin && k <= kmax)) {
-                float yk[CPL];
-                if (k == 1) {
-#pragma unroll
-                    for (int c = 0; c < CPL; ++c) yk[c] = yin[c];
-                } else {
-                    const float4 Y4 = L.y[p % WV_YS][lane];
-                    yk[0] = Y4.x; yk[1] = Y4.y; yk[2] = Y4.z; yk[3] = Y4.w;
-                }
-                float zn[CPL], xn[CPL], dx[CPL];
-                if (MODE == 1 && p == Q) {
-                    // virtual row below the plane: the dual of row Q - 1 gets z(Q) - z(Q - 1) = 0
-#pragma unroll
-                    for (int c = 0; c < CPL; ++c) { zn[c] = Sz[k - 1][c]; xn[c] = 0.f; dx[c] = 0.f; }
-                } else {
-                    wv_primal<EXACT>(a, xin, ui0, ui1, yk, Su0[k - 1], zn, xn, dx);
-                    if (k >= 3 && k <= NTRK + 2 && track && (k - 1) <= n - 2 && p >= qc0 && p < qc1) {
-#pragma unroll
-                        for (int c = 0; c < CPL; ++c) {
-                            if (EXACT) {
-                                const float d = xin[c] - xn[c];
-                                const float q = xn[c] + 1e-12f;
-                                tsd[k - 3] = __builtin_fmaf(d, d, tsd[k - 3]);
-                                tsn[k - 3] = __builtin_fmaf(q, q, tsn[k - 3]);
-                            } else {
-                                tsd[k - 3] = __builtin_fmaf(dx[c], dx[c], tsd[k - 3]);
-                                tsn[k - 3] = __builtin_fmaf(xn[c], xn[c], tsn[k - 3]);
-                            }
-                        }
-                    }
-                }
-                float un0[CPL], un1[CPL];
-                wv_dual<EXACT, true>(a, Su0[k - 1], Su1[k - 1], Sz[k - 1], zn, lastlane, un0, un1);
-#pragma unroll
-                for (int c = 0; c < CPL; ++c) {
-                    const float xo = Sx[k - 1][c];
-                    Sx[k - 1][c] = xn[c];
-                    Sz[k - 1][c] = zn[c];
-                    Su0[k - 1][c] = ui0[c];
-                    Su1[k - 1][c] = ui1[c];
-                    xin[c] = xo;
-                    ui0[c] = un0[c];
-                    ui1[c] = un1[c];
-                }
-            }
-        }
-        // ---------------- back: row t - n (x2^n = xin, u2^n = ui0 / ui1) ----------------
-        if (bk) {
-            float Xo[CPL];
-            if (ALPHA1) {
-#pragma unroll
-                for (int c = 0; c < CPL; ++c) Xo[c] = xin[c];
-            } else {
-                const float4 Y4 = L.y[bq_row % WV_YS][lane];
-                const float yy[CPL] = {Y4.x, Y4.y, Y4.z, Y4.w};
-#pragma unroll
-                for (int c = 0; c < CPL; ++c) Xo[c] = (1.0f - a.alpha) * yy[c] + a.alpha * xin[c];
-            }
-            float4 M4 = zero4, Q4 = zero4;
-            if (si.acc) {
-                float4 bm = zero4, bq = zero4;
-                if (need_prev) {
-                    wait_vm0();              // mean / sq of this row (issued at the step's front)
-                    bm = L.bm[lane];
-                    bq = L.bq[lane];
-                }
-                const float ms[CPL] = {bm.x, bm.y, bm.z, bm.w};
-                const float qs[CPL] = {bq.x, bq.y, bq.z, bq.w};
-                float m[CPL], qq[CPL];
-#pragma unroll
-                for (int c = 0; c < CPL; ++c) {
-                    if (si.first) {
-                        m[c] = si.cb * Xo[c];
-                        qq[c] = si.cb * (Xo[c] * Xo[c]);
-                    } else {
-                        m[c] = si.ca * ms[c] + si.cb * Xo[c];
-                        qq[c] = si.ca * qs[c] + si.cb * (Xo[c] * Xo[c]);
-                    }
-                }
-                M4 = make_float4(m[0], m[1], m[2], m[3]);
-                Q4 = make_float4(qq[0], qq[1], qq[2], qq[3]);
-                // the back staging read before the next step's DMA re-targets it
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            }
-            const size_t o = (size_t)bq_row * W;
-            const float4 X4 = make_float4(Xo[0], Xo[1], Xo[2], Xo[3]);
-            if (lane_ok) {
-                sgst16(xo_g + o, vo_s, X4);
-                sgst16(u2o_g + 2 * o, 2u * vo_s, make_float4(ui0[0], ui1[0], ui0[1], ui1[1]));
-                sgst16(u2o_g + 2 * o + 4, 2u * vo_s, make_float4(ui0[2], ui1[2], ui0[3], ui1[3]));
-                if (!ALPHA1) sgst16(x2o_g + o, vo_s, make_float4(xin[0], xin[1], xin[2], xin[3]));
-                if (accm_g) {
-                    sgst16(accm_g + o, vo_s, M4);
-                    sgst16(accq_g + o, vo_s, Q4);
-                }
-                if (smp_g) sgst16(smp_g + o, vo_s, X4);
-            }
-            nyoung += nst;
-        }
-    };
-
-    if (t_beg < t_fend) front_dma(t_beg);
-    int t = t_beg;
-    for (; t < min(t_st0, nsteps); ++t) do_step(t, WvMode<1>());
-    for (; t < t_st1; ++t) do_step(t, WvMode<0>());
-    for (; t < nsteps; ++t) do_step(t, WvMode<1>());
-    if (track) {
-        // the chain's rel-err sums of this range: iteration k's terms -> wred / norms (fp64)
-#pragma unroll
-        for (int k = 3; k <= NTRK + 2; ++k) {
-            if ((k - 1) <= n - 2) {
-                float d = wave_sum(lane_ok ? tsd[k - 3] : 0.f);
-                const float q = wave_sum(lane_ok ? tsn[k - 3] : 0.f);
-                if (!EXACT) d *= a.rho * a.rho;     // fast sums hold (x - x2_prev)^2
-                if (lane == 0) {
-                    const int it = k - 1;
-                    if (chain - c0g >= 0 && chain - c0g < WV_MAXC) {
-                        atomicAdd(&wred[chain - c0g][it][0], (double)d);
-                        atomicAdd(&wred[chain - c0g][it][1], (double)q);
-                    } else {
-                        atomicAdd(&a.norms[((size_t)chain * a.n_tv + it) * 2], (double)d);
-                        atomicAdd(&a.norms[((size_t)chain * a.n_tv + it) * 2 + 1], (double)q);
-                    }
-                }
-            }
-        }
-    }
-}
-
-template <bool EXACT, bool ALPHA1>
-__global__ void __launch_bounds__(WV_THREADS) tv_wave_kernel(const TvArgs a) {
-    __shared__ WaveShared sh;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long long step = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
-    const bool fresh = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
-    const int C = a.C;
-    const int g = (int)blockIdx.x * WV_NW + w;
-    // first chain of the workgroup's ranges: chains c0g .. c0g + WV_MAXC - 1 meet in LDS first
-    int c0g = 0;
-    {
-        int pl, pt, pts;
-        if (wave_item(a, (int)blockIdx.x * WV_NW, 0, pl, pt, pts)) c0g = pl / C;
-    }
-    for (int i = threadIdx.x; i < WV_MAXC * SP_MAXST * 2; i += blockDim.x) (&sh.wred[0][0][0])[i] = 0.0;
-    __syncthreads();
-    if (g < a.wv_slots) {
-        int pl, pt, pts;
-        for (int i = 0; wave_item(a, g, i, pl, pt, pts); ++i) {
-            RowMap rm;
-            part_rowmap(a.H, a.n_tv, pl, pt, pts, rm);
-            if (rm.Q > 0) wave_pass<EXACT, ALPHA1>(a, sh.w[w], rm, a.n_tv, true, step, fresh, sh.wred, c0g);
-        }
-    }
-    if (!a.fin_inline) return;            // main-pass-only launch (kernel timing): no side effects
-    __syncthreads();
-    for (int i = threadIdx.x; i < WV_MAXC * SP_MAXST; i += blockDim.x) {
-        const int gg = i / SP_MAXST, it = i - gg * SP_MAXST, ch = c0g + gg;
-        if (ch < a.B && it >= 2 && it <= a.n_tv - 2) {
-            const double d = sh.wred[gg][it][0], q = sh.wred[gg][it][1];
-            if (d != 0.0 || q != 0.0) {
-                atomicAdd(&a.norms[((size_t)ch * a.n_tv + it) * 2], d);
-                atomicAdd(&a.norms[((size_t)ch * a.n_tv + it) * 2 + 1], q);
-            }
-        }
-    }
-    // ---- step finalisation by the last workgroup to arrive (as tv_stream_kernel) ----
-    wait_vm0();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const int old = __hip_atomic_fetch_add(a.arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sh.s_flag = (old == (int)gridDim.x - 1) ? 1 : 0;
-        if (sh.s_flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    wait_vm0();
-    __syncthreads();
-    if (!sh.s_flag) return;
-    const int G = a.B;
-    for (int gg = threadIdx.x; gg < G; gg += blockDim.x) sh.s_stop[gg] = 0;
-    __syncthreads();
-    for (int i = threadIdx.x; i < G * SP_MAXST; i += blockDim.x) {
-        const int gg = i / SP_MAXST, t = i - gg * SP_MAXST;
-        if (t >= 2 && t <= a.n_tv - 2) {
-            const double nd = a.norms[((size_t)gg * a.n_tv + t) * 2];
-            const double nn = a.norms[((size_t)gg * a.n_tv + t) * 2 + 1];
-            const float rel = (float)sqrt(nd) / (float)sqrt(nn);
-            if (rel < a.tol) atomicOr(&sh.s_stop[gg], 1 << t);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) sh.s_item = 0;
-    __syncthreads();
-    for (int gg = threadIdx.x; gg < G; gg += blockDim.x) {
-        const int m = sh.s_stop[gg];
-        sh.s_stop[gg] = m ? (__ffs(m) - 1) + 1 : a.n_tv;
-        if (m) sh.s_item = 1;                 // some chain stopped early (benign race: all write 1)
-    }
-    __syncthreads();
-    if (sh.s_item) {
-        // rare: every plane of a stopped chain again with the stopped iteration count, split over the
-        // workgroup's waves (the step's inputs are intact: ping-pong state)
-        const int P = a.B * C;
-        for (int pl = 0; pl < P; ++pl) {
-            const int nstop = __builtin_amdgcn_readfirstlane(sh.s_stop[pl / C]);
-            if (nstop < a.n_tv) {
-                RowMap pm;
-                part_rowmap(a.H, a.n_tv, pl, w, WV_NW, pm);
-                if (pm.Q > 0) wave_pass<EXACT, ALPHA1>(a, sh.w[w], pm, nstop, false, step, fresh, sh.wred, c0g);
-            }
-        }
-        wait_vm0();
     }
     __syncthreads();
     for (int i = threadIdx.x; i < a.B * a.n_tv * 2; i += blockDim.x) a.norms[i] = 0.0;
@@ -2989,40 +2443,6 @@ __device__ __forceinline__ void bl_row_accumulate(const float* __restrict__ h, c
     }
 }
 
-#ifdef PSGLA_BLUR_PK
-// Experimental (build flag; bit-identical, measured in DESIGN section 3.3: the extra row copy costs
-// the registers of a third workgroup per CU, so it does not pay).  Packed form: acc pairs (columns k, k+1) and row pairs; {row[v], row[v+1]} for odd v comes from a copy of
-// the row shifted by one (register pairs must be even-aligned).  Same roundings, same order.
-typedef float bl_f2 __attribute__((ext_vector_type(2)));
-template <bool EXACT, int K, int M, int SEG>
-__device__ __forceinline__ void bl_row_accumulate_pk(const float* __restrict__ h, const float (&row)[SEG * 4], int ir,
-                                                     bl_f2 (&acc)[M][2]) {
-    bl_f2 re[SEG * 2], ro[SEG * 2 - 1];
-#pragma unroll
-    for (int j = 0; j < SEG * 2; ++j) { re[j].x = row[2 * j]; re[j].y = row[2 * j + 1]; }
-#pragma unroll
-    for (int j = 0; j < SEG * 2 - 1; ++j) { ro[j].x = row[2 * j + 1]; ro[j].y = row[2 * j + 2]; }
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-        const int u = ir - m;
-        if (u < 0 || u >= K) continue;
-#pragma unroll
-        for (int v = 0; v < K; ++v) {
-            const float hv = h[u * K + v];
-            const bl_f2 h2 = {hv, hv};
-            const bl_f2 p0 = (v & 1) ? ro[(v - 1) / 2] : re[v / 2];
-            const bl_f2 p1 = (v & 1) ? ro[(v + 1) / 2] : re[v / 2 + 1];
-            if (EXACT) {
-                acc[m][0] = acc[m][0] + h2 * p0;
-                acc[m][1] = acc[m][1] + h2 * p1;
-            } else {
-                acc[m][0] = __builtin_elementwise_fma(h2, p0, acc[m][0]);
-                acc[m][1] = __builtin_elementwise_fma(h2, p1, acc[m][1]);
-            }
-        }
-    }
-}
-#endif
 
 template <int SEG>
 __device__ __forceinline__ void bl_load_row(const float* p, float (&row)[SEG * 4]) {
@@ -3096,11 +2516,7 @@ __global__ void __launch_bounds__(BL_THREADS, (L <= 4 ? PSGLA_BLUR_WPE : 1)) blu
 #pragma unroll
         for (int m = 0; m < MR; ++m) {
             yv[m][0] = yv[m][1] = yv[m][2] = yv[m][3] = 0.f;
-#ifdef PSGLA_ABL_BLUR_NOLOAD
-            if (false) {
-#else
             if (p0 + m < BL_TH + 2 * L) {
-#endif
                 const float* yrow = yp + (size_t)wrap(tl.i0 - L + p0 + m, H) * W;
                 if (yvec) {
                     const float4 v = ld4(yrow + gj);
@@ -3118,7 +2534,6 @@ __global__ void __launch_bounds__(BL_THREADS, (L <= 4 ? PSGLA_BLUR_WPE : 1)) blu
     // for odd l / widths not a multiple of 4, element loads through registers.
     auto stage_x = [&](const Tile& tl, float* buf) {
         const float* xp = a.X + (size_t)tl.plane * HW;
-#ifndef PSGLA_ABL_BLUR_NOLOAD
         if (dma) {
 #pragma unroll
             for (int it = 0; it < NXI; ++it) {
@@ -3131,23 +2546,17 @@ __global__ void __launch_bounds__(BL_THREADS, (L <= 4 ? PSGLA_BLUR_WPE : 1)) blu
             }
             return;
         }
-#endif
         for (int n = t; n < XH * XQ; n += BL_THREADS) {
             const int p = n / XQ, qq = n - p * XQ;
             const float* rowp = xp + (size_t)wrap(tl.i0 - 2 * L + p, H) * W;
             const int gj = tl.j0 - 2 * L + 4 * qq;
             float4 v;
-#ifdef PSGLA_ABL_BLUR_NOLOAD
-            v = make_float4(0.f, 0.f, 0.f, (float)gj);   // diagnostic timing build only
-#else
             v.x = rowp[wrap(gj, W)]; v.y = rowp[wrap(gj + 1, W)];
             v.z = rowp[wrap(gj + 2, W)]; v.w = rowp[wrap(gj + 3, W)];
-#endif
             *reinterpret_cast<float4*>(&buf[4 * n]) = v;
         }
     };
 
-#ifndef PSGLA_BLUR_NOXCD
     // workgroups are dealt round-robin to the 8 XCDs: give each XCD a contiguous run of tiles so the
     // halo rows / columns a tile shares with its neighbours are re-read from the same L2 (-5 %; the
     // loads-and-stores floor 44 -> 31 us)
@@ -3158,9 +2567,6 @@ __global__ void __launch_bounds__(BL_THREADS, (L <= 4 ? PSGLA_BLUR_WPE : 1)) blu
         tid = xcd * qt + min(xcd, rt) + k;
     }
     const Tile tl = tile_of(tid);
-#else
-    const Tile tl = tile_of(blockIdx.x);
-#endif
     load_y(tl);                              // y first: it has landed by the time the tile has
     stage_x(tl, xs);
     wait_vm0();                              // this wave's x chunks and y landed
@@ -3170,34 +2576,14 @@ __global__ void __launch_bounds__(BL_THREADS, (L <= 4 ? PSGLA_BLUR_WPE : 1)) blu
         // r = A x - y
         if (rblk) {
             float acc[MR][4];
-#ifdef PSGLA_BLUR_PK
-            bl_f2 acc2[MR][2];
-#pragma unroll
-            for (int m = 0; m < MR; ++m) acc2[m][0] = acc2[m][1] = bl_f2{0.f, 0.f};
-#pragma unroll
-            for (int ir = 0; ir < MR + 2 * L; ++ir) {
-                float row[SEG * 4];
-                bl_load_row<SEG>(&xb[(p0 + ir) * XS + q], row);
-                bl_row_accumulate_pk<EXACT, K, MR, SEG>(a.hconv, row, ir, acc2);
-            }
-#pragma unroll
-            for (int m = 0; m < MR; ++m) {
-                acc[m][0] = acc2[m][0].x; acc[m][1] = acc2[m][0].y; acc[m][2] = acc2[m][1].x; acc[m][3] = acc2[m][1].y;
-            }
-#else
 #pragma unroll
             for (int m = 0; m < MR; ++m) acc[m][0] = acc[m][1] = acc[m][2] = acc[m][3] = 0.f;
 #pragma unroll
             for (int ir = 0; ir < MR + 2 * L; ++ir) {
                 float row[SEG * 4];
                 bl_load_row<SEG>(&xb[(p0 + ir) * XS + q], row);
-#ifndef PSGLA_ABL_BLUR_NOR
                 bl_row_accumulate<EXACT, K, MR, SEG>(a.hconv, row, ir, acc);
-#else
-                acc[0][ir & 3] += row[0];
-#endif
             }
-#endif
 #pragma unroll
             for (int m = 0; m < MR; ++m)
                 *reinterpret_cast<float4*>(&rs[(p0 + m) * RS + q]) =
@@ -3209,34 +2595,14 @@ __global__ void __launch_bounds__(BL_THREADS, (L <= 4 ? PSGLA_BLUR_WPE : 1)) blu
         const int j = tl.j0 + gq;
         if (j < W && tl.i0 + gp0 < H) {
             float acc[BL_MG][4];
-#ifdef PSGLA_BLUR_PK
-            bl_f2 acc2[BL_MG][2];
-#pragma unroll
-            for (int m = 0; m < BL_MG; ++m) acc2[m][0] = acc2[m][1] = bl_f2{0.f, 0.f};
-#pragma unroll
-            for (int ir = 0; ir < BL_MG + 2 * L; ++ir) {
-                float row[SEG * 4];
-                bl_load_row<SEG>(&rs[(gp0 + ir) * RS + gq], row);
-                bl_row_accumulate_pk<EXACT, K, BL_MG, SEG>(a.hcorr, row, ir, acc2);
-            }
-#pragma unroll
-            for (int m = 0; m < BL_MG; ++m) {
-                acc[m][0] = acc2[m][0].x; acc[m][1] = acc2[m][0].y; acc[m][2] = acc2[m][1].x; acc[m][3] = acc2[m][1].y;
-            }
-#else
 #pragma unroll
             for (int m = 0; m < BL_MG; ++m) acc[m][0] = acc[m][1] = acc[m][2] = acc[m][3] = 0.f;
 #pragma unroll
             for (int ir = 0; ir < BL_MG + 2 * L; ++ir) {
                 float row[SEG * 4];
                 bl_load_row<SEG>(&rs[(gp0 + ir) * RS + gq], row);
-#ifndef PSGLA_ABL_BLUR_NOG
                 bl_row_accumulate<EXACT, K, BL_MG, SEG>(a.hcorr, row, ir, acc);
-#else
-                acc[0][ir & 3] += row[0];
-#endif
             }
-#endif
 #pragma unroll
             for (int m = 0; m < BL_MG; ++m) {
                 const int i = tl.i0 + gp0 + m;
@@ -4021,30 +3387,6 @@ static int tile_geometry(int P, int H, int W, int h, int R, int* band_h, int* nb
     return ((P + 7) / 8) * 8 * nb;
 }
 
-// Row ranges of the per-wave pipeline kernel: one per wave slot (8 per CU).  P planes <= slots: plane p is
-// cut into base (+1 for the first `extra` planes) parts of >= 16 core rows each; more planes than slots:
-// whole planes, slot g taking planes g, g + slots, ...  Returns the number of slots (a multiple of WV_NW),
-// 0 if the shape does not fit (W > 256, W % 4, ldw != W, n_tv outside [1, 10], H < 2).
-static int wave_geometry(long long P, int H, int W, int ldw, int n_tv, TvArgs* a) {
-    if (W > TV_COLS || (W & 3) || ldw != W || n_tv < 1 || n_tv > SP_MAXST || H < 2) return 0;
-    const long long slots = (long long)device_cus() * WV_NW;
-    int whole = 0, base = 1, extra = 0;
-    long long used;
-    if (P >= slots) {
-        whole = 1;
-        used = slots;
-    } else {
-        const long long maxparts = H / 16 > 1 ? H / 16 : 1;
-        base = (int)(slots / P);
-        extra = (int)(slots % P);
-        if (base >= maxparts) { base = (int)maxparts; extra = 0; }
-        used = P * base + extra;
-    }
-    used = (used + WV_NW - 1) / WV_NW * WV_NW;
-    if (a) { a->wv_slots = (int)used; a->wv_base = base; a->wv_extra = extra; a->wv_whole = whole; }
-    return (int)used;
-}
-
 // Column segments of the streaming kernel: equal core widths (multiples of 4) cut from the image
 // width W; segment s's wave covers columns [f0, f0 + 256) with f0 = (cc0 - h) & ~3 (cc0 = s * seg_w),
 // which must reach cc1 + h for interior cuts (the TV dependency cone) and the row pitch L at the
@@ -4073,18 +3415,6 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
     const int P = a.B * a.C;
     if (mask == 0) mask = 3;
     if (mask & 1) {
-        if (FRONT == FRONT_INPAINT && a.wave) {
-            TvArgs s = a;
-            s.fin_inline = (mask & 2) ? 1 : 0;
-            hipLaunchKernelGGL((tv_wave_kernel<EXACT, ALPHA1>), dim3(s.wv_slots / WV_NW), dim3(WV_THREADS), 0, st, s);
-            return launch_check("tv_wave_kernel");
-        }
-        if (FRONT == FRONT_INPAINT && a.tile_r > 0 && a.msteps > 1) {
-            if (!ALPHA1 || a.tile_r != 3 || mask != 3) return fail(0, "psgla_tv_step: multi_steps needs alpha == 1 and a full launch");
-            const int grid = ((P + 7) / 8) * 8 * a.nbands;
-            hipLaunchKernelGGL((tv_tile_multi_kernel<EXACT, 3>), dim3(grid), dim3(TV_THREADS), 0, st, a);
-            return launch_check("tv_tile_multi_kernel");
-        }
         if (FRONT == FRONT_INPAINT && a.tile_r > 0) {
             TvArgs s = a;
             s.fin_inline = (mask & 2) ? 1 : 0;
@@ -4100,17 +3430,17 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
             s.fin_inline = (mask & 2) ? 1 : 0;
             const int grid = s.split_wgs > 0 ? s.split_wgs : P * s.st_nsegs;   // virtual planes
             const bool gen = !(s.ldw == s.W && s.st_nsegs == 1);
-            if (s.p2p) {
-                if (!gen)
-                    hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1, false, true>), dim3(grid), dim3(TV_THREADS), 0, st, s);
-                else
-                    hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1, true, true>), dim3(grid), dim3(TV_THREADS), 0, st, s);
-            } else {
-                if (!gen)
-                    hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1, false, false>), dim3(grid), dim3(TV_THREADS), 0, st, s);
-                else
-                    hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1, true, false>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+            if constexpr (ALPHA1) {
+                if (s.pair) {
+                    if (gen) return fail(0, "psgla_tv_step: row-pair kernel on a padded / segmented shape");
+                    hipLaunchKernelGGL((tv_pair_kernel<EXACT>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+                    return launch_check("tv_pair_kernel");
+                }
             }
+            if (!gen)
+                hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1, false>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+            else
+                hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1, true>), dim3(grid), dim3(TV_THREADS), 0, st, s);
             int rc = launch_check("tv_stream_kernel");
             if (rc) return rc;
             return 0;                    // finalised in-kernel (or main pass only)
@@ -4151,7 +3481,13 @@ static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
     a.stream = streamable && d->kernel_variant != 1;
     if ((d->kernel_variant == 2 || d->kernel_variant == 3) && !streamable)
         { g_sel_err = "psgla_tv_step: shape not supported by the streaming kernel"; return -1; }
-    a.p2p = d->kernel_variant == 3 ? 1 : 0;
+    if (d->kernel_variant < 0 || d->kernel_variant > 4)
+        { g_sel_err = "psgla_tv_step: kernel_variant outside 0..4"; return -1; }
+    // row-pair pipeline: one 256-column window (W <= 256, W % 4 == 0, no row padding), alpha == 1
+    const bool pairable = streamable && a.ldw == a.W && a.W <= TV_COLS && d->x2[0] == nullptr && d->n_tv >= PR_NZ;
+    if (d->kernel_variant == 3 && !pairable)
+        { g_sel_err = "psgla_tv_step: shape not supported by the row-pair kernel (W <= 256, W % 4 == 0, alpha == 1, n_tv >= 3)"; return -1; }
+    a.pair = pairable && d->kernel_variant == 3 ? 1 : 0;     // forced only: measured slower
     // small-batch tile kernel: forced (variant 4) or, in auto mode, when all tiles fit in one round
     // on the CUs (a row stream would be mostly pipeline fill: strong scaling's 64/N chains per GPU)
     a.tile_r = 0;
@@ -4167,19 +3503,8 @@ static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
             a.nsegs = 1;
             a.tiles = nb;
             a.stream = 0;
+            a.pair = 0;
         }
-    }
-    // per-wave pipeline kernel: forced (variant 5)
-    a.wave = 0;
-    if (d->kernel_variant == 5) {
-        if (wave_geometry((long long)d->B * d->C, d->H, d->W, a.ldw, d->n_tv, &a) == 0)
-            { g_sel_err = "psgla_tv_step: shape not supported by the wave kernel"; return -1; }
-        a.wave = 1;
-        a.split_wgs = 0;
-        a.st_nsegs = 1;
-        a.stream = 0;
-        a.tile_r = 0;
-        return 4;
     }
     if (!a.stream && a.tile_r == 0 && a.ldw != a.W) { g_sel_err = "psgla_tv_step: a row pitch ldw != W needs the streaming kernel"; return -1; }
     a.split_wgs = 0;
@@ -4193,7 +3518,7 @@ static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
         }
     }
     if (a.tile_r > 0) return 3;
-    if (a.stream) return a.p2p ? 2 : 1;
+    if (a.stream) return a.pair ? 2 : 1;
     return 0;
 }
 
@@ -4231,20 +3556,10 @@ int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream) {
     a.fresh_dev = d->fresh; a.per_chain_norm = 1; a.norms = d->norms; a.arrive = d->arrive;
     a.it0 = 0; a.last_chunk = 1; a.stopped = nullptr;
     a.advance_step = d->advance_step;
-    a.stamps = (unsigned long long*)d->debug_stamps;
     a.n_inter = s->n_inter; a.nm = s->n_inter_mmse; a.coef = s->acc_coef;
     a.samples = s->samples; a.samples_cap = s->samples_cap;
     a.blocks = s->blocks; a.blocks2 = s->blocks2; a.blocks_cap = s->blocks_cap;
     if (select_step_kernel(d, a) < 0) return g_sel_err == g_err ? (int)hipErrorInvalidValue : fail(0, g_sel_err);
-    if (d->multi_steps > 1) {
-        // persistent multi-step tile kernel: every tile co-resident (grid barrier), alpha == 1
-        if (a.tile_r != 3 || !alpha1 || !d->norms_ring || (d->launch_mask != 0 && d->launch_mask != 3))
-            return fail(0, "psgla_tv_step: multi_steps > 1 needs the tile kernel, alpha == 1, norms_ring and a full launch");
-        const long long grid = ((long long)(d->B * d->C + 7) / 8) * 8 * a.nbands;
-        if (grid > device_cus()) return fail(0, "psgla_tv_step: multi_steps > 1 needs every tile resident (grid > CUs)");
-        a.msteps = d->multi_steps;
-        a.norms_ring = d->norms_ring;
-    }
     hipStream_t st = (hipStream_t)stream;
     const int m = d->launch_mask;
     if (d->exact)

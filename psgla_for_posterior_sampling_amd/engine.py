@@ -1,7 +1,7 @@
 """Batched, graph-replayable PSGLA engines over the fused HIP steps.
 
 ``FusedTvChains`` runs B independent PSGLA chains (inpainting fidelity + warm-started TV
-prox) with one fused kernel launch (+ one small finaliser) per Langevin step:
+prox) with one fused kernel launch per Langevin step (the band kernel adds a small finaliser):
 restoration_algorithms.py:231-271 with the closures of sampling_images.py:295 and the
 deepinv TVDenoiser of sampling_images.py:138.  All step-dependent quantities (noise
 counter, block coefficients, sample / block slots, ping-pong parity) are derived on the
@@ -19,13 +19,17 @@ from . import _native as N
 from . import hip_ops as K
 
 
+# PsglaTvStep.kernel_variant (include/psgla_hip.h)
+KERNEL_VARIANTS = {"auto": 0, "band": 1, "stream": 2, "pair": 3, "tile": 4}
+
+
 class FusedTvChains:
     def __init__(self, init: torch.Tensor, y: torch.Tensor, mask_u8: torch.Tensor, *, c1: float, c2: float,
                  sigma2: float, alpha: float, ths: float, tv: K.TvConstants, seed: int, n_iter: int,
                  n_inter: int, n_inter_mmse: int, chain0: int = 0, exact: bool = False,
                  tv_x2: torch.Tensor | None = None, tv_u2: torch.Tensor | None = None,
                  store_samples: bool = True, store_blocks: bool = True, kernel_variant: str = "auto",
-                 stream_wgs: int = 0, multi_step: bool = False):
+                 stream_wgs: int = 0):
         if init.dim() != 4:
             raise ValueError("init must be (B, C, H, W)")
         if tv.n_it > N.TV_MAX_FUSED_IT:
@@ -37,7 +41,9 @@ class FusedTvChains:
         # rows padded to a multiple of 4 columns so that every width runs on the streaming kernel
         # (psgla_kernels.hip: ldw); the padding columns are scratch and every result is a view
         # of the first W columns
-        self.ldw = Wd if (Wd % 4 == 0 or kernel_variant in ("band", "tile", "wave")) else (Wd + 3) // 4 * 4
+        if kernel_variant not in KERNEL_VARIANTS:
+            raise ValueError(f"kernel_variant must be one of {sorted(KERNEL_VARIANTS)}")
+        self.ldw = Wd if (Wd % 4 == 0 or kernel_variant in ("band", "tile", "pair")) else (Wd + 3) // 4 * 4
         self.pshape = (B, C, H, self.ldw)
         self.device = dev
         self.alpha = float(alpha)
@@ -88,11 +94,9 @@ class FusedTvChains:
         d.fresh = self.work.fresh.data_ptr()
         d.norms = self.work.norms.data_ptr()
         d.arrive = self.work.arrive.data_ptr()
-        d.norms_ring = self.work.norms_ring.data_ptr()
-        d.kernel_variant = {"auto": 0, "band": 1, "stream": 2, "p2p": 3, "tile": 4, "wave": 5}[kernel_variant]
+        d.kernel_variant = KERNEL_VARIANTS[kernel_variant]
         d.stream_wgs = int(stream_wgs)
         self.desc = d
-        self.multi_step = bool(multi_step)
         self.sched_struct = self.sched.struct(True, 0)
         if self.warm_first:
             # first step of a warm-started run: the TV primal x2 (previous run's state) is not X
@@ -133,33 +137,17 @@ class FusedTvChains:
                 self._launch(self.desc)
             self.steps_done += 1
 
-    @property
-    def multi_step_active(self) -> bool:
-        """Graph segments run as ONE persistent multi-step launch (tv_tile_multi_kernel):
-        opt-in (multi_step=True; measured slower than one tile-kernel launch per step), when the tile kernel
-        is selected with every tile resident and alpha == 1."""
-        if not (self.multi_step and self.alpha1) or self.main_kernel != "tv_tile_kernel":
-            return False
-        B, C, H, _ = self.shape
-        bands = -(-H // (48 - 2 * self.desc.n_tv)) if H > 48 else 1
-        return -(-(B * C) // 8) * 8 * bands <= torch.cuda.get_device_properties(self.device).multi_processor_count
-
     def capture(self, steps_per_graph: int):
         """Capture `steps_per_graph` identical steps into one hipGraph (after step 0): one launch per
-        step, or one persistent launch for all of them (multi_step_active)."""
+        step."""
         if self.steps_done == 0 and self.warm_first:
             self.step(1)
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=s):
-            if steps_per_graph > 1 and self.multi_step_active:
-                dm = N.PsglaTvStep.from_buffer_copy(self.desc)
-                dm.multi_steps = steps_per_graph
-                self._launch(dm)
-            else:
-                for _ in range(steps_per_graph):
-                    self._launch(self.desc)
+            for _ in range(steps_per_graph):
+                self._launch(self.desc)
         torch.cuda.current_stream().wait_stream(s)
         self.graph = g
         self.graph_steps = steps_per_graph
@@ -182,16 +170,41 @@ class FusedTvChains:
         self.sched.d_step.fill_(step)
         self.steps_done = step
 
+    def snapshot(self) -> dict:
+        """Device copies of everything a step reads or advances (chain / TV state, live accumulators, the
+        step counter, the TV restart flag) -- for benchmarking: replays after a snapshot can be undone by
+        restore() (samples / block means already written stay written)."""
+        torch.cuda.current_stream().synchronize()
+        bufs = {"x": self.x, "u2": self.u2, "mean": self.mean, "sq": self.sq}
+        if self.x2 is not None:
+            bufs["x2"] = self.x2
+        snap = {k: [t.clone() for t in v] for k, v in bufs.items()}
+        snap["d_step"] = self.sched.d_step.clone()
+        snap["fresh"] = self.work.fresh.clone()
+        snap["steps_done"] = self.steps_done
+        return snap
+
+    def restore(self, snap: dict):
+        torch.cuda.current_stream().synchronize()
+        for k in ("x", "u2", "mean", "sq", "x2"):
+            if k in snap:
+                for dst, src in zip(getattr(self, k), snap[k]):
+                    dst.copy_(src)
+        self.sched.d_step.copy_(snap["d_step"])
+        self.work.fresh.copy_(snap["fresh"])
+        self.steps_done = snap["steps_done"]
+
     @property
     def main_kernel(self) -> str:
         """Name of the kernel psgla_tv_step dispatches for this shape (the library's own choice,
         psgla_tv_step_kernel: the small-batch tile kernel when its tiles fit on the CUs at once, else
-        the row stream for W % 4 == 0 rows -- always, the engine pads rows --, 1 <= n_tv <= 10,
-        H >= 2; the band kernel otherwise or when forced)."""
+        the row-pair pipeline for unpadded rows of <= 256 columns at alpha == 1, else the row stream
+        (W % 4 == 0 rows -- always, the engine pads rows --, 1 <= n_tv <= 10, H >= 2); the band
+        kernel otherwise or when forced)."""
         k = N.lib().psgla_tv_step_kernel(ctypes.byref(self.desc))
         if k < 0:
             raise RuntimeError(N.lib().psgla_last_error().decode())
-        return ("tv_main_kernel", "tv_stream_kernel", "tv_stream_kernel", "tv_tile_kernel", "tv_wave_kernel")[k]
+        return ("tv_main_kernel", "tv_stream_kernel", "tv_pair_kernel", "tv_tile_kernel")[k]
 
     def launch_main_only(self, n: int = 1):
         """Launch only the fused tile kernel n times for the CURRENT step (idempotent: it reads

@@ -351,7 +351,5 @@ class TvWorkspace:
 
     def __init__(self, groups: int, n_it: int, device):
         self.norms = torch.zeros((max(groups, 1), max(n_it, 1), 2), dtype=torch.float64, device=device)
-        # the persistent multi-step kernel's sums of steps s % 3 == 1, 2 (PsglaTvStep.norms_ring)
-        self.norms_ring = torch.zeros((2, max(groups, 1), max(n_it, 1), 2), dtype=torch.float64, device=device)
         self.arrive = torch.zeros(4, dtype=torch.int32, device=device)
         self.fresh = torch.zeros(4, dtype=torch.int32, device=device)

@@ -188,7 +188,7 @@ def _fused_batch(B, chain0, exact, n_iter=40, H=48, W=64, alpha=1.0, variant="au
     return eng, (dg, y, init, mask2d, c1, c2)
 
 
-@pytest.mark.parametrize("variant", ["stream", "band"])
+@pytest.mark.parametrize("variant", ["stream", "pair", "band"])
 def test_fused_chains_independent_of_batching_and_graph(variant):
     """Chain k's trajectory depends only on (seed, global chain id): B=4 batch vs B=2 batch
     with chain0=2, and eager vs hipGraph replay -- bit-identical (multi-GPU sharding property)."""
@@ -205,7 +205,8 @@ def test_fused_chains_independent_of_batching_and_graph(variant):
 
 
 @pytest.mark.parametrize("variant,H,W", [("stream", 48, 64), ("band", 48, 64), ("stream", 70, 300),
-                                          ("band", 70, 300), ("auto", 37, 29)])
+                                          ("band", 70, 300), ("auto", 37, 29), ("pair", 48, 64), ("pair", 37, 28),
+                                          ("pair", 21, 256)])
 def test_fused_multichain_exact_vs_oracle(variant, H, W):
     B = 3
     eng, (dg, y, init, mask2d, c1, c2) = _fused_batch(B, 10, exact=True, n_iter=30, H=H, W=W, variant=variant)
@@ -237,14 +238,16 @@ def _oracle_chain(init, dg, n_iter, chain):
     return _ORACLE_CACHE[key]
 
 
+@pytest.mark.parametrize("variant", ["stream", "pair"])
 @pytest.mark.parametrize("stream_wgs", [-1, 3, 4, 7, 11, 20, 97])
-def test_stream_row_split_exact_vs_oracle(stream_wgs):
+def test_stream_row_split_exact_vs_oracle(stream_wgs, variant):
     """Row-split streaming (the plane rows of all chains cut into stream_wgs ranges, n_tv halo rows
-    at cuts inside a plane, ranges spanning plane boundaries): bit-identical to the checker for
-    every cut position; -1 = one workgroup per plane."""
+    at cuts inside a plane, ranges spanning plane boundaries, odd row counts for the row-pair
+    pipeline): bit-identical to the checker for every cut position; -1 = one workgroup per plane."""
     B, H, W, n_iter = 3, 48, 64, 20
     eng, (dg, y, init, mask2d, c1, c2) = _fused_batch(B, 10, exact=True, n_iter=n_iter, H=H, W=W,
-                                                      variant="stream", stream_wgs=stream_wgs)
+                                                      variant=variant, stream_wgs=stream_wgs)
+    assert eng.main_kernel == ("tv_pair_kernel" if variant == "pair" else "tv_stream_kernel")
     eng.run(n_iter, graph_steps=0)
     torch.cuda.synchronize()
     bm, bm2 = eng.blocks()
@@ -267,8 +270,9 @@ class _RecordingTV(orc.TVDenoiser):
         return out
 
 
+@pytest.mark.parametrize("variant", ["stream", "pair"])
 @pytest.mark.parametrize("stream_wgs", [0, -1])
-def test_stream_early_stop_exact_vs_oracle(stream_wgs):
+def test_stream_early_stop_exact_vs_oracle(stream_wgs, variant):
     """tol large enough that deepinv's early stop fires in some steps: the stream kernel's last
     workgroup re-streams the stopped chains' planes with k+1 iterations -- bit-identical."""
     from psgla_for_posterior_sampling_amd.engine import FusedTvChains
@@ -281,7 +285,7 @@ def test_stream_early_stop_exact_vs_oracle(stream_wgs):
     eng = FusedTvChains(init.expand(B, -1, -1, -1).contiguous().to(DEV), y.to(DEV), mask2d.to(torch.uint8).to(DEV),
                         c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)), alpha=1.0,
                         ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10, tol=tol), seed=4,
-                        n_iter=n_iter, n_inter=3, n_inter_mmse=2, exact=True, kernel_variant="stream",
+                        n_iter=n_iter, n_inter=3, n_inter_mmse=2, exact=True, kernel_variant=variant,
                         stream_wgs=stream_wgs)
     eng.run(n_iter, graph_steps=0)
     torch.cuda.synchronize()
@@ -330,7 +334,7 @@ def test_fused_full_size_fast_vs_exact():
     dg, y, init, mask2d, _ = inpainting_problem(x)
     c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
     outs = []
-    for exact, variant in ((True, "stream"), (False, "stream"), (True, "band")):
+    for exact, variant in ((True, "stream"), (False, "stream"), (True, "band"), (True, "pair"), (False, "pair")):
         eng = FusedTvChains(init.expand(64, -1, -1, -1).contiguous(), y, dg.mask_u8, c1=c1, c2=c2,
                             sigma2=dg.sigma2, alpha=1.0, ths=float(np.float32(10 / 255.0)),
                             tv=K.TvConstants(n_it_max=10), seed=0, n_iter=12, n_inter=10, n_inter_mmse=10,
@@ -338,8 +342,10 @@ def test_fused_full_size_fast_vs_exact():
         eng.run(12, graph_steps=0)
         torch.cuda.synchronize()
         outs.append((eng.X.clone(), eng.blocks()[0].clone()))
-    (xe, be), (xf, bf), (xb, bb) = outs
-    assert torch.equal(xe, xb) and torch.equal(be, bb)      # both exact kernels agree bit for bit
+    (xe, be), (xf, bf), (xb, bb), (xpe, bpe), (xpf, bpf) = outs
+    assert torch.equal(xe, xb) and torch.equal(be, bb)      # the exact kernels agree bit for bit
+    assert torch.equal(xe, xpe) and torch.equal(be, bpe)
+    assert torch.equal(xf, xpf) and torch.equal(bf, bpf)    # fast: the same per-element arithmetic
     assert torch.isfinite(xf).all() and torch.isfinite(xe).all()
     assert rel(bf.cpu().numpy(), be.cpu().numpy()) < REL_TOL_MEAN
     assert rel(xf.cpu().numpy(), xe.cpu().numpy()) < 1e-4
@@ -687,16 +693,19 @@ def test_stream_segmented_early_stop_exact_vs_oracle():
     assert fired, "test needs the early stop to fire"
 
 
-# ------------------------------------------------------------------------------ P2P pipeline
-@pytest.mark.parametrize("exact,H,W,alpha,stream_wgs,tol,B", [
-    (True, 48, 64, 1.0, 0, 1e-5, 3), (True, 48, 64, 1.0, 7, 1e-5, 3), (True, 48, 64, 1.0, -1, 1e-5, 3),
-    (False, 48, 64, 1.0, 11, 1e-5, 3), (True, 70, 300, 1.0, 0, 1e-5, 2), (True, 37, 29, 0.6, 5, 1e-5, 3),
-    (True, 40, 52, 1.0, 0, 3e-2, 2), (False, 256, 256, 1.0, 0, 1e-5, 16)])
-def test_p2p_pipeline_equals_barrier_pipeline(exact, H, W, alpha, stream_wgs, tol, B):
-    """The stream kernel with point-to-point LDS progress waits (kernel_variant "p2p") computes exactly
-    what the barrier-synchronised pipeline computes (itself bit-identical to the oracle above): same
-    samples, block means, TV state, for row splits, column segments (W > 256, padded rows), alpha != 1,
-    early stops (tol 3e-2) and a full-size batch; no progress wait ever timed out (arrive[1] == 0)."""
+# ------------------------------------------------------------------------------ row-pair pipeline
+@pytest.mark.parametrize("exact,H,W,stream_wgs,tol,B,n_tv", [
+    (True, 48, 64, 0, 1e-5, 3, 10), (True, 48, 64, 7, 1e-5, 3, 10), (True, 48, 64, -1, 1e-5, 3, 10),
+    (False, 48, 64, 11, 1e-5, 3, 10), (True, 37, 28, 5, 1e-5, 3, 10), (True, 40, 52, 0, 3e-2, 2, 10),
+    (True, 33, 256, 3, 1e-5, 2, 10), (True, 48, 64, 0, 1e-5, 3, 3), (True, 48, 64, 6, 1e-5, 3, 4),
+    (True, 2, 16, 0, 1e-5, 2, 10), (False, 256, 256, 0, 1e-5, 16, 10), (True, 256, 256, 0, 1e-5, 8, 10)])
+def test_pair_pipeline_equals_stream_pipeline(exact, H, W, stream_wgs, tol, B, n_tv):
+    """The row-pair pipeline (tv_pair_kernel: two rows per pipeline step, single-slot rings between a
+    dual phase and a primal phase) computes exactly what the one-row stream kernel computes (itself
+    bit-identical to the oracle): same samples, block means and TV state, for row splits with halo cuts,
+    odd row counts (a dummy row closes the last pair), narrow images (idle lanes), full-width rows,
+    early stops (tol 3e-2: the last workgroup re-streams stopped planes), 3 <= n_tv < 10 (idle stage waves),
+    H = 2 and full-size batches, in graph replay."""
     from psgla_for_posterior_sampling_amd.engine import FusedTvChains
     from psgla_for_posterior_sampling_amd import hip_ops as K
     g = torch.Generator().manual_seed(8)
@@ -704,19 +713,38 @@ def test_p2p_pipeline_equals_barrier_pipeline(exact, H, W, alpha, stream_wgs, to
     dg, y, init, mask2d = orc.inpainting_problem(x, seed_ip=1)
     c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
     outs = []
-    for variant in ("stream", "p2p"):
+    for variant in ("stream", "pair"):
         eng = FusedTvChains(init.expand(B, -1, -1, -1).contiguous().to(DEV), y.to(DEV),
                             mask2d.to(torch.uint8).to(DEV), c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
-                            alpha=alpha, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10, tol=tol),
+                            alpha=1.0, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=n_tv, tol=tol),
                             seed=3, n_iter=24, n_inter=5, n_inter_mmse=4, exact=exact, kernel_variant=variant,
                             stream_wgs=stream_wgs)
+        assert eng.main_kernel == ("tv_pair_kernel" if variant == "pair" else "tv_stream_kernel")
         eng.run(24, graph_steps=8)
         torch.cuda.synchronize()
-        assert int(eng.work.arrive[1].item()) == 0, "a P2P progress wait timed out"
+        assert int(eng.sched.d_step.item()) == 24 and int(eng.work.arrive[0].item()) == 0
+        assert float(eng.work.norms.abs().sum()) == 0.0
         bm, bm2 = eng.blocks()
         outs.append((eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone()))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_auto_dispatch_by_shape():
+    """64 chains x 3 x 256 x 256 (BASELINE configs[1], one GPU): auto dispatch picks the row stream; 8 chains
+    (the 8-GPU strong split) the tile kernel; alpha != 1 and padded rows the row stream."""
+    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+
+    def kern(B, H, W, alpha=1.0):
+        z = torch.zeros((B, 3, H, W), device=DEV)
+        return FusedTvChains(z, z[:1].clone(), torch.ones((H, W), dtype=torch.uint8, device=DEV), c1=0.1, c2=0.1,
+                             sigma2=1e-5, alpha=alpha, ths=0.04, tv=K.TvConstants(n_it_max=10), seed=0, n_iter=10,
+                             n_inter=10, n_inter_mmse=10, store_samples=False, store_blocks=False).main_kernel
+    assert kern(64, 256, 256) == "tv_stream_kernel"
+    assert kern(8, 256, 256) == "tv_tile_kernel"
+    assert kern(64, 256, 256, alpha=0.6) == "tv_stream_kernel"
+    assert kern(16, 321, 481) == "tv_stream_kernel"
 
 
 # ------------------------------------------------------------------------------ small-batch tile kernel
@@ -811,110 +839,3 @@ def test_tile_kernel_early_stop_handoff_full_size(tol):
     for a, b in zip(outs[("stream", tol)], outs[("tile", tol)]):
         assert torch.equal(a, b)
     assert not torch.equal(outs[("tile", tol)][3], outs[("tile", 1e-5)][3]), "no early stop fired"
-
-
-@pytest.mark.parametrize("exact,tol", [(False, 1e-5), (True, 1e-5), (False, 3e-3), (True, 1e-3)])
-def test_tile_multi_step_equals_per_step_full_size(exact, tol):
-    """The persistent multi-step tile kernel (one launch per 10-step graph segment, core-row state resident
-    in registers / LDS across steps, grid barrier between steps, every workgroup deciding deepinv's early
-    stop) against one tile-kernel launch per step: 8 chains at 3 x 256 x 256, 40 steps, samples, block
-    means, final X and u2 bit-identical, with and without firing early stops; no barrier wait timed out."""
-    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
-    from psgla_for_posterior_sampling_amd import hip_ops as K
-    B = 8
-    g = torch.Generator(device=DEV).manual_seed(31)
-    xs = torch.rand((B, 3, 256, 256), generator=g, device=DEV)
-    gen = torch.Generator(device=DEV).manual_seed(0)
-    mask2d = (torch.rand((256, 256), generator=gen, device=DEV) > 0.5).to(torch.uint8)
-    y = mask2d.float() * xs + torch.normal(torch.zeros_like(xs), std=(1 / 255.0) * torch.ones_like(xs),
-                                           generator=gen)
-    init = (mask2d.float() * y + (1 - mask2d.float()) * 0.5).contiguous()
-    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
-    outs = []
-    runs = [(True, tol), (False, tol)] + ([(True, 1e-5)] if tol > 1e-5 else [])
-    for multi, t in runs:
-        eng = FusedTvChains(init, y.contiguous(), mask2d, c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
-                            alpha=1.0, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10, tol=t),
-                            seed=0, n_iter=41, n_inter=10, n_inter_mmse=10, exact=exact, multi_step=multi)
-        assert eng.multi_step_active == multi
-        eng.step(1)                       # eager first step (fresh TV start), then 4 graph segments
-        eng.capture(10)
-        eng.replay(4)
-        torch.cuda.synchronize()
-        assert int(eng.work.arrive[3].item()) == 0, "grid barrier wait timed out"
-        assert int(eng.sched.d_step.item()) == 41
-        assert float(eng.work.norms.abs().sum()) == 0.0 and float(eng.work.norms_ring.abs().sum()) == 0.0
-        bm, bm2 = eng.blocks()
-        outs.append((eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone()))
-    for a, b in zip(outs[0], outs[1]):
-        assert torch.equal(a, b)
-    if len(outs) > 2:
-        assert not torch.equal(outs[0][3], outs[2][3]), "no early stop fired"
-
-
-@pytest.mark.parametrize("B,H,W,alpha,tol,n_tv", [
-    (3, 48, 64, 1.0, 1e-5, 10),      # 3 ranges per plane: halo cuts at both ends
-    (2, 100, 64, 1.0, 1e-5, 10),     # 6 ranges per plane
-    (2, 77, 40, 0.6, 1e-5, 10),      # alpha != 1 (x2 state), narrow image (idle lanes)
-    (2, 40, 52, 1.0, 0.03, 10),      # deepinv's early stop (recompute by the last workgroup)
-    (2, 90, 256, 1.0, 1e-5, 3),      # n_tv < 10: general step body only
-    (1, 30, 20, 1.0, 1e-5, 7),       # whole planes (H < 32)
-])
-def test_wave_kernel_exact_vs_oracle(B, H, W, alpha, tol, n_tv):
-    """The per-wave pipeline kernel (each wave runs front, all inner iterations and back of its own row
-    range, state in registers) in exact mode: samples, block means and TV state bit-identical to the
-    CPU oracle for halo cuts inside planes, alpha != 1, early stop, n_tv < 10 and whole-plane ranges."""
-    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
-    from psgla_for_posterior_sampling_amd import hip_ops as K
-    g = torch.Generator().manual_seed(11)
-    x = torch.rand((1, 3, H, W), generator=g)
-    dg, y, init, mask2d = orc.inpainting_problem(x, seed_ip=4)
-    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
-    n_iter = 14
-    eng = FusedTvChains(init.expand(B, -1, -1, -1).contiguous().to(DEV), y.to(DEV), mask2d.to(torch.uint8).to(DEV),
-                        c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)), alpha=alpha,
-                        ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=n_tv, tol=tol), seed=8,
-                        n_iter=n_iter, n_inter=3, n_inter_mmse=2, chain0=2, exact=True, kernel_variant="wave")
-    assert eng.main_kernel == "tv_wave_kernel"
-    eng.run(n_iter, graph_steps=6)
-    torch.cuda.synchronize()
-    bm, bm2 = eng.blocks()
-    for b in range(B):
-        tv = orc.TVDenoiser(n_it_max=n_tv, tol=tol)
-        Xl, Ml, M2l = orc.psgla(init, dg, tv, torch.tensor(alpha), torch.tensor(10.0), sig_float=10 / 255.0,
-                                delta=(10 / 255.0) ** 2, n_iter=n_iter, n_inter=3, n_inter_mmse=2, seed=8, chain=2 + b)
-        np.testing.assert_array_equal(eng.samples()[:, b].cpu().numpy(), np.stack([t.numpy() for t in Xl]))
-        np.testing.assert_array_equal(bm[:, b].cpu().numpy(), np.stack([t.numpy() for t in Ml]))
-        np.testing.assert_array_equal(bm2[:, b].cpu().numpy(), np.stack([t.numpy() for t in M2l]))
-        np.testing.assert_array_equal(eng.x2_state[b].cpu().numpy(), tv.x2.numpy()[0])
-        np.testing.assert_array_equal(eng.u2_state[b].cpu().numpy(), tv.u2.numpy()[0])
-
-
-@pytest.mark.parametrize("B,H,W", [(64, 256, 256), (4, 256, 256), (720, 32, 32)])
-def test_wave_kernel_equals_stream_kernel(B, H, W):
-    """The benched geometry (64 chains x 3 x 256 x 256: 2048 ranges of ~24 rows), a small batch (16
-    ranges per plane) and more planes than wave slots (whole planes, several per wave): the wave kernel
-    and the row-streaming kernel give bit-identical chains in both arithmetic modes."""
-    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
-    from psgla_for_posterior_sampling_amd import hip_ops as K
-    g = torch.Generator(device=DEV).manual_seed(4321)
-    xs = torch.rand((B, 3, H, W), generator=g, device=DEV)
-    gen = torch.Generator(device=DEV).manual_seed(0)
-    mask2d = (torch.rand((H, W), generator=gen, device=DEV) > 0.5).to(torch.uint8)
-    y = mask2d.float() * xs + torch.normal(torch.zeros_like(xs), std=(1 / 255.0) * torch.ones_like(xs),
-                                           generator=gen)
-    init = (mask2d.float() * y + (1 - mask2d.float()) * 0.5).contiguous()
-    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
-    for exact in (True, False):
-        outs = []
-        for variant in ("stream", "wave"):
-            eng = FusedTvChains(init, y.contiguous(), mask2d, c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
-                                alpha=1.0, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10), seed=0,
-                                n_iter=24, n_inter=10, n_inter_mmse=10, exact=exact, kernel_variant=variant)
-            eng.run(24, graph_steps=12)
-            torch.cuda.synchronize()
-            bm, bm2 = eng.blocks()
-            outs.append((eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone()))
-            del eng
-        for a, b in zip(*outs):
-            assert torch.equal(a, b), f"exact={exact}"
