@@ -16,7 +16,21 @@ Differences, all outside the hot path:
   (architectures restated in denoisers.py) load deepinv-format weights from --weights_dir
   (``--allow_random_weights`` runs random-init networks for plumbing tests);
 * extra flags: --datasets_root, --weights_dir, --results_root, --no_plots,
-  --allow_random_weights, --graph_steps.
+  --allow_random_weights, --graph_steps, --batch_size, --tv_restart.
+
+Batched and multi-GPU runs (build-specific; BASELINE configs 4-5 run CBSD68 over 8 GPUs).  Every image
+is one Langevin chain whose noise is keyed by (--seed_alg, chain id); the chain id of image i is its rank
+in the dataset listing stably sorted by image shape (= i for a dataset of one shape, e.g. set1c), so a
+chain's samples do not depend on how images are batched or sharded.  ``--batch_size B`` groups the
+images of one shape, in listing order, into batches of up to B chains that run as ONE psgla / pnpula
+call ((B, C, H, W) state); under ``torch.distributed.run`` the image indices [indx_start, n) are split
+contiguously over the ranks (one GPU per rank: cuda:(gpu_number + LOCAL_RANK)), each rank runs its
+share, and rank 0 gathers every image's record and writes the reference's im_i/ directories.
+TV warm start: the reference carries the TV prox state (x2, u2) from image k to image k+1
+(sampling_images.py:138, reused in the :265 loop); that is kept for --batch_size 1 on one rank.  A
+batched or sharded run starts the TV prox fresh for every image (x2 = Y, u2 = 0, as the reference
+does for its first image); ``--tv_restart`` makes a sequential run do the same, which is the run a
+batched one equals.  DnCNN / DRUNet have no state across images.
 """
 from __future__ import annotations
 
@@ -29,7 +43,7 @@ import torch
 
 from . import metrics
 from .denoisers import DenoiserPrior, DnCNN, DRUNet, TVDenoiser
-from .fidelity import deblurring_problem, inpainting_problem
+from .fidelity import BlurFidelity, InpaintingFidelity, deblurring_problem, inpainting_problem
 from .restoration_algorithms import pnpula, psgla
 
 
@@ -68,6 +82,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--no_plots", action="store_true")
     p.add_argument("--allow_random_weights", action="store_true")
     p.add_argument("--graph_steps", type=int, default=None)
+    p.add_argument("--batch_size", type=int, default=1, help="chains (images of one shape) per psgla call")
+    p.add_argument("--tv_restart", action="store_true", help="fresh TV prox state for every image")
     return p
 
 
@@ -127,6 +143,9 @@ def algorithm_parameters(pars, argv):
 def make_denoiser(pars, device):
     if pars.den == "TV":
         return TVDenoiser(n_it_max=pars.den_TV_it)
+    # random-init networks (--allow_random_weights, plumbing runs) are seeded: every rank of a sharded run
+    # and every run of a comparison build the same network
+    torch.manual_seed(pars.seed_alg)
     if pars.den == "DnCNN":
         w = os.path.join(pars.weights_dir, "dncnn_sigma2_lipschitz_color.pth")
         if not os.path.exists(w) and not pars.allow_random_weights:
@@ -149,50 +168,85 @@ def read_image(path: str) -> np.ndarray:
     return im[..., :3]
 
 
-def restore_image(pars, argv, im: np.ndarray, denoiser, device, path_result_im: str):
-    """One image of the reference's loop (sampling_images.py:265-529)."""
-    N, s, lambd, delta, n_inter, ex = algorithm_parameters(pars, argv)
-    n_inter_mmse = int(np.copy(n_inter))
-    dtype = torch.float32
-    alphat = torch.tensor(pars.alpha, dtype=dtype, device=device)
+def _problem(pars, im: np.ndarray, device):
+    """The inverse problem of one image (sampling_images.py:283-341), its generator seeded per image as in
+    the reference: (data term, y_t (1, C, H, W), init (1, C, H, W), mask_2d or None, mask or None)."""
     if pars.grayscale:
         im_t = torch.from_numpy(np.ascontiguousarray(im)).float().unsqueeze(0).unsqueeze(0).to(device)
     else:
         im_t = torch.from_numpy(np.transpose(np.ascontiguousarray(im), (2, 0, 1))).float().unsqueeze(0).to(device)
-    mask = None
     if pars.Pb == "inpainting":
         data_grad, y_t, init_torch, mask_2d, mask = inpainting_problem(im_t, seed_ip=pars.seed_ip, prop=pars.prop,
                                                                        sigma=pars.sigma)
-    elif pars.Pb == "deblurring":
+        return data_grad, y_t, init_torch, mask_2d, mask
+    if pars.Pb == "deblurring":
         data_grad, y_t, init_torch = deblurring_problem(im_t, seed_ip=pars.seed_ip, l=pars.l,
                                                         blur_type=pars.blur_type, si=pars.si, sigma=pars.sigma)
+        return data_grad, y_t, init_torch, None, None
+    raise ValueError("unknown --Pb " + pars.Pb)
+
+
+def restore_batch(pars, argv, ims, chain0: int, denoiser, device):
+    """The reference's per-image loop body (sampling_images.py:265-470) for len(ims) images of one shape
+    run as ONE chain batch (chain ids chain0 ..): returns [(record, extras, mask)] per image.  With one
+    image this is exactly the reference's run of that image."""
+    N, s, lambd, delta, n_inter, ex = algorithm_parameters(pars, argv)
+    n_inter_mmse = int(np.copy(n_inter))
+    dtype = torch.float32
+    alphat = torch.tensor(pars.alpha, dtype=dtype, device=device)
+    probs = [_problem(pars, im, device) for im in ims]
+    B = len(ims)
+    y_b = torch.cat([p[1] for p in probs], dim=0).contiguous()
+    init_b = torch.cat([p[2] for p in probs], dim=0).contiguous()
+    if B == 1:
+        data_grad = probs[0][0]
+    elif pars.Pb == "inpainting":
+        # one shape, one seed_ip: every image of the batch has the same mask (sampling_images.py:285-290)
+        data_grad = InpaintingFidelity(probs[0][3], y_b, probs[0][0].sigma2)
     else:
-        raise ValueError("unknown --Pb " + pars.Pb)
+        f0 = probs[0][0]
+        data_grad = BlurFidelity(f0.hconv, f0.hcorr, f0.l, y_b, f0.sigma2t)
     name = "sigma{}_s{}".format(pars.sigma, int(255 * s))
     lambdt = torch.tensor(lambd, dtype=dtype, device=device)
     kw = dict(seed=pars.seed_alg, device=device, n_iter=N, n_inter=n_inter, n_inter_mmse=n_inter_mmse,
-              path=path_result_im, save_images_online=pars.save_images_online, name=name)
+              path=pars._path_im, save_images_online=pars.save_images_online, name=name, chain0=chain0)
+    if pars.graph_steps is not None:
+        kw["graph_steps"] = pars.graph_steps
     if pars.alg == "psgla":
-        if pars.graph_steps is not None:
-            kw["graph_steps"] = pars.graph_steps
-        Samples_t, Mmse_t, Mmse2_t = psgla(init=init_torch, data_grad=data_grad, denoiser=denoiser, alpha=alphat,
+        Samples_t, Mmse_t, Mmse2_t = psgla(init=init_b, data_grad=data_grad, denoiser=denoiser, alpha=alphat,
                                            lambd=lambdt, sig_float=s, delta=delta, **kw)
     else:
         s1, s2t = ex["s1"], torch.tensor(ex["s2"], dtype=dtype, device=device)
         prior_grad = DenoiserPrior(denoiser, s1, alphat, s2t)    # alphat*(D(x, s1) - x)/s2t (:156-157)
-        if pars.graph_steps is not None:
-            kw["graph_steps"] = pars.graph_steps
-        Samples_t, Mmse_t, Mmse2_t = pnpula(init=init_torch, data_grad=data_grad, prior_grad=prior_grad,
+        Samples_t, Mmse_t, Mmse2_t = pnpula(init=init_b, data_grad=data_grad, prior_grad=prior_grad,
                                             delta=torch.tensor(delta, dtype=dtype, device=device), lambd=lambdt,
                                             **kw)
-    record, extras = metrics.analyse_run(im, Samples_t, Mmse_t, Mmse2_t, y_t, init_torch, pars.grayscale)
-    record.update({"n_iter": N, "s": s, "alpha": pars.alpha, "c_min": 0, "c_max": 1, "sigma": pars.sigma,
-                   "l": pars.l, "lambda": lambd, "delta": delta})
+    out = []
+    for b, im in enumerate(ims):
+        pick = (lambda lst: [t[b] for t in lst]) if B > 1 else (lambda lst: lst)   # noqa: E731
+        record, extras = metrics.analyse_run(im, pick(Samples_t), pick(Mmse_t), pick(Mmse2_t), probs[b][1],
+                                             probs[b][2], pars.grayscale)
+        record.update({"n_iter": N, "s": s, "alpha": pars.alpha, "c_min": 0, "c_max": 1, "sigma": pars.sigma,
+                       "l": pars.l, "lambda": lambd, "delta": delta})
+        out.append((record, extras, probs[b][4], name))
+    return out
+
+
+def restore_image(pars, argv, im: np.ndarray, denoiser, device, path_result_im: str, chain: int = 0):
+    """One image of the reference's loop (sampling_images.py:265-529), results written to path_result_im."""
+    pars._path_im = path_result_im
+    record, extras, mask, name = restore_batch(pars, argv, [im], chain, denoiser, device)[0]
+    write_result(pars, path_result_im, name, record, mask)
+    return record, extras
+
+
+def write_result(pars, path_result_im: str, name: str, record: dict, mask):
+    """sampling_images.py:470 (the result dict) and the images of :523-535."""
+    os.makedirs(path_result_im, exist_ok=True)
     np.save(path_result_im + "/" + name + "_result.npy", record)
     if not pars.no_plots:
         _save_images(pars, path_result_im, name, record, mask)
     print("The output PSNR : {:.2f} dB / output SSIM : {:.2f}".format(record["PSNR_MMSE"], record["SIM_MMSE"]))
-    return record, extras
 
 
 def _save_images(pars, path, name, rec, mask):
@@ -210,25 +264,119 @@ def _save_images(pars, path, name, rec, mask):
         plt.imsave(path + "/error.png", np.clip(m * (rec["MMSE"] - rec["ground_truth"]), 0, 1), cmap=cmap)
 
 
+def dataset_files(pars):
+    input_path = os.path.join(pars.datasets_root, pars.dataset_name)
+    return [os.path.join(input_path, f) for f in sorted(os.listdir(input_path))]
+
+
+def image_shape(path: str):
+    from PIL import Image
+    with Image.open(path) as im:
+        return im.size[::-1]
+
+
+def chain_ids(files):
+    """Chain id of every image: its rank in the listing stably sorted by image shape (module docstring)."""
+    order = sorted(range(len(files)), key=lambda i: (image_shape(files[i]), i))
+    ids = [0] * len(files)
+    for r, i in enumerate(order):
+        ids[i] = r
+    return ids
+
+
+def shape_batches(indices, files, ids, batch_size: int):
+    """Batches of up to batch_size images of one shape with consecutive chain ids, in listing order of
+    their first image."""
+    groups = {}
+    for i in indices:
+        groups.setdefault(image_shape(files[i]), []).append(i)
+    batches = []
+    for g in groups.values():
+        cur = []
+        for i in g:
+            if cur and (len(cur) == batch_size or ids[i] != ids[cur[-1]] + 1):
+                batches.append(cur)
+                cur = []
+            cur.append(i)
+        if cur:
+            batches.append(cur)
+    return sorted(batches, key=lambda b: b[0])
+
+
+def load_image(pars, path: str) -> np.ndarray:
+    im_int = read_image(path)
+    im = np.float32(im_int / 255.)
+    if pars.grayscale:
+        im = np.float32(im_int[..., 0] / 255.)
+    return im
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else list(argv)
     pars = build_parser().parse_args(argv)
     if pars.alg not in ("psgla", "pnp_ula"):
         raise NotImplementedError(f"--alg {pars.alg}: only psgla and pnp_ula are part of this build")
-    device = torch.device("cuda:" + str(pars.gpu_number))
-    path_result = result_path(pars, argv)
+    if pars.batch_size < 1:
+        raise ValueError("--batch_size must be >= 1")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")          # per-image records only: no collective on the hot path
+    ndev = max(torch.cuda.device_count(), 1)
+    device = torch.device("cuda:" + str((pars.gpu_number + local) % ndev))
+    sequential = world == 1 and pars.batch_size == 1
+    if pars.save_images_online and not sequential:
+        raise ValueError("--save_images_online needs a sequential run (--batch_size 1, one rank)")
+    path_result = result_path(pars, argv) if rank == 0 else None
+    if world > 1:
+        dist.barrier()
+        path_result = result_path(pars, argv)
+    files = dataset_files(pars)
+    ids = chain_ids(files)
+    indices = list(range(pars.indx_start, len(files)))
     denoiser = make_denoiser(pars, device)   # one object for the whole dataset, as the reference (:138)
-    input_path = os.path.join(pars.datasets_root, pars.dataset_name)
-    files = sorted(os.listdir(input_path))
+    if sequential:
+        records = []
+        for i in indices:
+            path_result_im = os.path.join(path_result, "im_" + str(i))
+            os.makedirs(path_result_im, exist_ok=True)
+            if pars.tv_restart and isinstance(denoiser, TVDenoiser):
+                denoiser.restart = True
+            records.append(restore_image(pars, argv, load_image(pars, files[i]), denoiser, device, path_result_im,
+                                         chain=ids[i])[0])
+        return records
+    from .sharding import chain_range
+    a, b = chain_range(len(indices), world, rank)
+    mine = indices[a:b]
+    local_out = {}
+    pars._path_im = ""
+    for batch in shape_batches(mine, files, ids, pars.batch_size):
+        if isinstance(denoiser, TVDenoiser):
+            denoiser.restart = True              # batched / sharded: fresh TV state for every image
+        ims = [load_image(pars, files[i]) for i in batch]
+        for i, (record, _extras, mask, name) in zip(batch, restore_batch(pars, argv, ims, ids[batch[0]], denoiser,
+                                                                           device)):
+            local_out[i] = (record, None if mask is None else mask.cpu(), name)
+    if world > 1:
+        import torch.distributed as dist
+        parts = [None] * world
+        dist.all_gather_object(parts, local_out)
+        gathered = {}
+        for d in parts:
+            gathered.update(d)
+    else:
+        gathered = local_out
     records = []
-    for i in range(pars.indx_start, len(files)):
-        path_result_im = os.path.join(path_result, "im_" + str(i))
-        os.makedirs(path_result_im, exist_ok=True)
-        im_int = read_image(os.path.join(input_path, files[i]))
-        im = np.float32(im_int / 255.)
-        if pars.grayscale:
-            im = np.float32(im_int[..., 0] / 255.)
-        records.append(restore_image(pars, argv, im, denoiser, device, path_result_im)[0])
+    if rank == 0:
+        for i in indices:
+            record, mask, name = gathered[i]
+            write_result(pars, os.path.join(path_result, "im_" + str(i)), name, record, mask)
+            records.append(record)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
     return records
 
 

@@ -125,3 +125,20 @@ def test_result_path_scheme(tmp_path):
     path = SI.result_path(p.parse_args(argv), argv)
     assert path == os.path.join(str(tmp_path), "images", "inpainting", "prop_0.5", "set1c", "psgla", "TV", "N_1000")
     assert os.path.isdir(path)
+
+
+def test_cli_chain_ids_and_shape_batches(tmp_path):
+    """Batched CLI bookkeeping (CPU): chain id = rank in the listing stably sorted by shape; batches hold
+    images of one shape with consecutive chain ids, at most batch_size of them."""
+    from PIL import Image
+    d = tmp_path / "ds"
+    d.mkdir()
+    shapes = [(24, 32), (24, 32), (32, 24), (24, 32), (32, 24), (24, 32)]
+    for i, (h, w) in enumerate(shapes):
+        Image.fromarray(np.zeros((h, w, 3), np.uint8)).save(str(d / f"{i:03d}.png"))
+    files = [str(d / f) for f in sorted(os.listdir(str(d)))]
+    ids = SI.chain_ids(files)
+    assert ids == [0, 1, 4, 2, 5, 3]
+    assert SI.shape_batches(list(range(6)), files, ids, 2) == [[0, 1], [2, 4], [3, 5]]
+    assert SI.shape_batches(list(range(6)), files, ids, 8) == [[0, 1, 3, 5], [2, 4]]
+    assert SI.shape_batches([1, 2, 3], files, ids, 8) == [[1, 3], [2]]
