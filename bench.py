@@ -29,7 +29,7 @@ from a snapshot taken before them: the timed steps are exactly those of a run th
 for W steps, on every rank, whatever the wall-clock warm-up ran.
 
 The roofline figure divides the algorithmic bytes of one launch by the dominant kernel's
-(tv_pair_kernel at 64 chains per GPU: one launch per step) average duration from HIP events recorded on the
+(tv_stream_kernel at 64 chains per GPU, tv_tile_kernel at 8: one launch per step) average duration from HIP events recorded on the
 replay stream around the timed region; the kernel re-launched alone on its own stream is
 reported beside it (kernel_ms_isolated) as a cross-check.  `traffic` (HBM bytes per launch
 from rocprofv3 PMC counters) cannot be collected inside an un-profiled run: it is read from
@@ -53,7 +53,6 @@ METRIC = "Langevin steps/sec (3×256×256, batch=64) at 1/2/4/8 GPU; HBM GB/s vs
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # committed PMC summaries (tools/profile_round.sh + tools/pmc_summary.py) by dominant kernel
 PMC_PROFILES = {"tv_stream_kernel": os.path.join("profiles", "r02e_pmc_tv_stream.json"),
-                "tv_pair_kernel": os.path.join("profiles", "r03_pmc_tv_pair.json"),
                 "tv_tile_kernel": os.path.join("profiles", "r02e_pmc_tv_tile.json")}
 
 
@@ -73,7 +72,7 @@ def parse():
     p.add_argument("--kernel-iters", type=int, default=50)
     p.add_argument("--tv-iters", type=int, default=10, help="TV n_it_max (analysis only; the workload is 10)")
     p.add_argument("--stream-wgs", type=int, default=0, help="stream kernel work split (0 auto, -1 per plane)")
-    p.add_argument("--variant", choices=["auto", "band", "stream", "pair", "tile"], default="auto",
+    p.add_argument("--variant", choices=["auto", "band", "stream", "tile"], default="auto",
                    help="fused TV kernel (analysis; auto = the library's choice)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the batch-1 CPU leg")
     p.add_argument("--cpu-b64-steps", type=int, default=10, help="timed steps of the batch-64 CPU leg (0: skip)")

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PSGLA_HIP_ABI_VERSION 6
+#define PSGLA_HIP_ABI_VERSION 7
 
 /* Max inner TV iterations the fused (temporally blocked) kernel handles. */
 #define PSGLA_TV_MAX_FUSED_IT 24
@@ -76,9 +76,6 @@ typedef struct PsglaSchedule {
  *     48-row tiles all fit on the CUs at once (few chains per GPU): ONE launch; its last
  *     workgroup to finish evaluates the early stop, recomputes stopped chains and advances
  *     the step (no second kernel);
- *   - else the row-pair pipeline (tv_pair_kernel: W <= 256, W % 4 == 0, ldw == W,
- *     alpha == 1 i.e. x2 == NULL, 1 <= n_tv <= 10, H >= 2): two rows per pipeline step,
- *     ONE launch, finalised in-kernel the same way;
  *   - else the row-streaming kernel (tv_stream_kernel: row pitch ldw % 4 == 0,
  *     1 <= n_tv <= 10, H >= 2, every width with column segments, any alpha): one row per
  *     pipeline step, ONE launch, finalised in-kernel;
@@ -114,9 +111,9 @@ typedef struct PsglaTvStep {
     int32_t launch_mask;      /* 0 or 3: both kernels; 1: tile kernel only (re-runs the same step:
                                  idempotent, for kernel timing); 2: finaliser only            */
     int32_t kernel_variant;   /* 0: auto (see above); 1: force the band kernel; 2: force the row stream
-                                 (one row per pipeline step); 3: force the row-pair pipeline (W <= 256,
-                                 W % 4 == 0, ldw == W, alpha == 1); 4: force the small-batch tile kernel
-                                 (W <= 256, W % 4 == 0, ldw == W).  Other values are rejected. */
+                                 (one row per pipeline step); 4: force the small-batch tile kernel
+                                 (W <= 256, W % 4 == 0, ldw == W).  Other values (3 included: the
+                                 row-pair pipeline of ABI 6 is gone) are rejected. */
     int32_t stream_wgs;       /* streaming kernel work split: 0 auto (rows of all planes cut into
                                  one contiguous range per CU, n_tv halo rows at cuts, when W <= 256);
                                  -1 one workgroup per plane; > 0 force that many row ranges      */
@@ -130,8 +127,8 @@ typedef struct PsglaTvStep {
 
 int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream);
 /* Which kernel psgla_tv_step launches for this descriptor (host-side query, launches nothing):
- * 0 band kernel + finaliser, 1 row stream (tv_stream_kernel), 2 row-pair pipeline (tv_pair_kernel),
- * 3 small-batch tile kernel (tv_tile_kernel); -1 if the descriptor is rejected. */
+ * 0 band kernel + finaliser, 1 row stream (tv_stream_kernel), 3 small-batch tile kernel
+ * (tv_tile_kernel); -1 if the descriptor is rejected.  (2 is unused since ABI 7.) */
 int psgla_tv_step_kernel(const PsglaTvStep* d);
 
 /* ---------------------------------------------------------------------------------

@@ -97,7 +97,6 @@ struct TvArgs {
     int st_nsegs, st_seg_w, st_halo;  // stream kernel column segmentation (W > 256)
     int fin_inline;                 // stream kernel: 1 = the last workgroup finalises the step
     int tile_r;                     // > 0: small-batch tile kernel with tile_r rows per wave (one tile per workgroup)
-    int pair;                       // stream kernel: 1 = the row-pair pipeline (tv_pair_kernel)
 };
 
 // Inner iterations (chunk-local) whose rel_err deepinv tests: global index >= 2 ("it > 1"); in the call's
@@ -1440,530 +1439,6 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
         *a.arrive = 0;
         if (a.fresh_dev) *a.fresh_dev = 0;
         if (a.advance_step && a.d_step) *a.d_step = *a.d_step + 1;   // (re-read: the start-of-kernel value measured +0.5 % here)
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-// Row-PAIR pipeline (tv_pair_kernel): the fused PSGLA + TV step with TWO rows per pipeline step.
-//
-// The row-stream pipeline above spends ~1,660 cycles per row step for ~780 cycles of VALU work per
-// SIMD: every wave's per-step chain (LDS read -> dependent VALU -> LDS write) is exposed once per row
-// and the SIMDs idle between the bursts.  Here every role handles a row PAIR
-// per step -- two independent dependency chains per wave, half the steps per row -- and the steps are
-// split into two phases so that each LDS ring needs ONE slot of two rows (two-slot rings of row
-// pairs do not fit in 160 KB):
-//   W-phase  stage k: dual update of the row pair (a-3, a-2) (all inputs in registers), written to
-//                     ring k; front: its finished pair written to ring 0 and to the Y ring
-//   barrier
-//   C-phase  stage k: reads ring k-1 = rows (a, a+1) (written in this step's W-phase), primal update
-//                     of both; front / back: noise, data term, loads, accumulators, stores
-//   barrier
-// with a = 2t - 3k + 3 for stage k at step t (stage k+1 trails stage k by 3 rows; the front hands
-// rows (2t, 2t+1) to stage 1 at step t; the back takes rows (2t - 3n, 2t - 3n + 1) from ring n).
-// A ring slot written in W_t is read in C_t and next written in W_{t+1}, after the C_t barrier.
-// The per-element arithmetic is the row stream's (stage_phase_a / stage_phase_b, the same data term
-// and accumulators): exact mode is bit-identical to the oracle, fast mode to the fast row stream.
-// Shape: one 256-column window (W <= 256, W % 4 == 0, rows unpadded), alpha == 1 (X == x2); the same
-// row split over the CUs (build_rowmap), per-chain early stop and in-kernel finalisation.
-// ---------------------------------------------------------------------------------------
-constexpr int PR_YRING = 30;      // Y rows kept from the front (step r/2) to the last stage (step (r+27)/2)
-constexpr int PR_ZRING = 4;       // noise of 4 row pairs (written 2 steps before the front consumes it)
-constexpr int PR_NZ = 3;          // stage waves 1..3 also generate the Langevin noise (n_tv >= 3)
-constexpr int PR_T0 = -6;         // first step: noise of pair 0 starts at step -5
-
-struct PairShared {
-    float4 x2[SP_MAXST + 1][2][WAVE];     // ring k (k = 0: front): the row pair handed to stage k + 1
-    float4 u0[SP_MAXST + 1][2][WAVE];
-    float4 u1[SP_MAXST + 1][2][WAVE];
-    float4 y[PR_YRING][WAVE];             // Y rows (prox anchor), by stream row % 30
-    float4 z[PR_ZRING][2][WAVE];          // Langevin noise Z of a row pair, by pair % 4
-    float4 fst[SP_FRONT][2][4][WAVE];     // front LDS-DMA staging of its next pair: X, y, u2 lo, u2 hi
-    uint32_t fmk[SP_FRONT][2][WAVE];      // mask bytes (4 columns per lane)
-    float4 bst[SP_BACK][2][2][2][WAVE];   // back staging [buffer][row][mean, sq]
-    float red[SP_MAXSEG][SP_MAXST][2];
-};
-
-__device__ __forceinline__ int pr_yslot(int r) { return (r + 32 * PR_YRING) % PR_YRING; }   // r >= -960
-
-// stream row q starts a segment (the stream's first row, or a plane start inside a split range)
-__device__ __forceinline__ bool seg_start(const RowMap& m, int q) {
-    return q == 0 || (m.ns > 1 && q == m.q1) || (m.ns > 2 && q == m.q2) || (m.ns > 3 && q == m.q3);
-}
-
-// Langevin noise of stream row q (Philox of the lane's quad; W % 4 == 0, so a lane's 4 columns are one quad
-// of the chain's C*H*W image) -- in three pieces: Philox, Box-Muller of outputs 0-1, of outputs 2-3.  The
-// state is a lane's 4 words, Philox outputs first, then the normals' bits in place.
-__device__ __forceinline__ void noise_philox(const TvArgs& a, const RowMap& rm, int q, long long step, int gj0,
-                                             uint32_t (&nz)[4]) {
-    RowCursor c;
-    cursor_init(rm, c, min(max(q, 0), rm.Q - 1));
-    const int bb = c.p / a.C, cc = c.p - bb * a.C;
-    const size_t e = ((size_t)cc * a.H + c.r) * a.W + gj0;
-    uint32_t c0 = (uint32_t)(e >> 2), c1 = (uint32_t)step, c2 = TAG_LANGEVIN, c3 = (uint32_t)(a.seed >> 32);
-    philox4x32_10(c0, c1, c2, c3, (uint32_t)a.seed, (uint32_t)(a.chain0 + bb));
-    nz[0] = c0; nz[1] = c1; nz[2] = c2; nz[3] = c3;
-}
-template <int h>
-__device__ __forceinline__ void noise_bm(uint32_t (&nz)[4]) {
-    float z0, z1;
-    box_muller(nz[2 * h], nz[2 * h + 1], z0, z1);
-    nz[2 * h] = __float_as_uint(z0);
-    nz[2 * h + 1] = __float_as_uint(z1);
-}
-
-// Stage k over the steps [T0, T1): see the section comment for the schedule.  Three row states
-// rotate (prev | pair): after C_t, `prev` holds row a-1 and the pair rows a, a+1; the next W-phase
-// duals rows a-1 and a (z of a and a+1 known) and the pair's second row becomes `prev`.  Stages
-// 1..PR_NZ also generate the noise of one row pair every PR_NZ steps (a piece per phase).
-template <bool EXACT, bool TRK>
-__device__ __forceinline__ void pair_stage(const TvArgs& a, PairShared& sh, const RowMap& rm, int k, int T0,
-                                           int T1, int lane, int lastk, bool core, long long stepi) {
-    const int Q = rm.Q;
-    const int qc0 = rm.htop, qc1 = Q - rm.hbot;
-    const float zero[CPL] = {0.f, 0.f, 0.f, 0.f};
-    StageRow R0, R1, R2;
-    float lsd = 0.f, lsn = 0.f;          // rel-err partial sums of segment sacc (core rows)
-    int sacc = 0;
-    const bool nzw = k <= PR_NZ;         // a noise wave
-    uint32_t nza[4] = {0u, 0u, 0u, 0u}, nzb[4] = {0u, 0u, 0u, 0u};
-    auto flush = [&]() __attribute__((always_inline)) {
-        if (TRK) {
-            float d = wave_sum(core ? lsd : 0.f);
-            const float q = wave_sum(core ? lsn : 0.f);
-            if (!EXACT) d *= a.rho * a.rho;          // fast sums hold (x - x2_prev)^2
-            if (lane == 0) { sh.red[sacc][k - 1][0] = d; sh.red[sacc][k - 1][1] = q; }
-            lsd = 0.f; lsn = 0.f;
-        }
-    };
-    // dual update of row r (state d, z of the row below in zb) -> ring k slot s
-    auto dual = [&](int r, const StageRow& d, const StageRow& zb, int s) __attribute__((always_inline)) {
-        if (r < 0 || r >= Q) return;
-        float un0[CPL], un1[CPL];
-        if (r + 1 < Q && !seg_start(rm, r + 1)) stage_phase_b<EXACT, true>(a, d, zb.z, lastk, un0, un1);
-        else stage_phase_b<EXACT, false>(a, d, zero, lastk, un0, un1);   // the segment's last row
-        sh.x2[k][s][lane] = make_float4(d.x2n[0], d.x2n[1], d.x2n[2], d.x2n[3]);
-        sh.u0[k][s][lane] = make_float4(un0[0], un0[1], un0[2], un0[3]);
-        sh.u1[k][s][lane] = make_float4(un1[0], un1[1], un1[2], un1[3]);
-    };
-    // primal update of row r from ring k-1 slot s (u0 of the row above in pa)
-    auto primal = [&](int r, const float4& X2, const float4& U0, const float4& U1, const float4& YY,
-                      const StageRow& pa, StageRow& o) __attribute__((always_inline)) {
-        if (r < 0 || r >= Q) return;
-        const bool fs = seg_start(rm, r);
-        if (TRK && fs && r > 0) { flush(); ++sacc; }
-        float rd = 0.f, rn = 0.f;
-        // u0 of the row above (none at a segment start); selected by value: two call sites fed
-        // `zero` / pa.u0 get merged over a pointer select into scratch memory
-        float pu[CPL];
-#pragma unroll
-        for (int kk = 0; kk < CPL; ++kk) pu[kk] = fs ? 0.f : pa.u0[kk];
-        stage_phase_a<EXACT, TRK>(a, X2, U0, U1, YY, pu, o, rd, rn);
-        if (TRK && r >= qc0 && r < qc1) { lsd += rd; lsn += rn; }
-    };
-    // noise duty (stage k <= PR_NZ): pair p = t + 5 - pi with p = k - 1 (mod PR_NZ), piece pi of 3 per phase:
-    //   pi 0: Philox of rows a / b (W / C), 1: Box-Muller 0-1, 2: Box-Muller 2-3, then Z of pair p to LDS
-    // (the row's state is picked at compile time: a runtime-selected array reference goes to scratch)
-    auto noise = [&](int t, auto phc) __attribute__((always_inline)) {
-        constexpr int ph = decltype(phc)::value;
-        if (!nzw) return;
-        const int pi = ((t + 5 - (k - 1)) % PR_NZ + PR_NZ) % PR_NZ;
-        const int p = t + 5 - pi;
-        if (p < 0 || 2 * p >= Q) return;
-        if constexpr (ph == 0) {
-            if (pi == 0) noise_philox(a, rm, 2 * p, stepi, CPL * lane, nza);
-            else if (pi == 1) noise_bm<0>(nza);
-            else noise_bm<1>(nza);
-        } else {
-            if (pi == 0) noise_philox(a, rm, 2 * p + 1, stepi, CPL * lane, nzb);
-            else if (pi == 1) noise_bm<0>(nzb);
-            else noise_bm<1>(nzb);
-        }
-        if (ph == 1 && pi == 2) {
-            sh.z[p & (PR_ZRING - 1)][0][lane] = make_float4(__uint_as_float(nza[0]), __uint_as_float(nza[1]),
-                                                            __uint_as_float(nza[2]), __uint_as_float(nza[3]));
-            sh.z[p & (PR_ZRING - 1)][1][lane] = make_float4(__uint_as_float(nzb[0]), __uint_as_float(nzb[1]),
-                                                            __uint_as_float(nzb[2]), __uint_as_float(nzb[3]));
-        }
-    };
-    // one step with the roles (prev P | pair A, B): W duals P (row a-3) and A (row a-2), C reads rows
-    // a, a+1 into P and A (the new pair; B becomes prev)
-    auto step = [&](int t, StageRow& P, StageRow& A, StageRow& B) __attribute__((always_inline)) {
-        const int r = 2 * t - 3 * k + 3;
-        dual(r - 3, P, A, 0);
-        dual(r - 2, A, B, 1);
-        noise(t, std::integral_constant<int, 0>());
-        lds_barrier();
-        if (r + 1 >= 0 && r < Q) {
-            const float4 X2a = sh.x2[k - 1][0][lane], U0a = sh.u0[k - 1][0][lane], U1a = sh.u1[k - 1][0][lane];
-            const float4 X2b = sh.x2[k - 1][1][lane], U0b = sh.u0[k - 1][1][lane], U1b = sh.u1[k - 1][1][lane];
-            const float4 Ya = sh.y[pr_yslot(r)][lane], Yb = sh.y[pr_yslot(r + 1)][lane];
-            primal(r, X2a, U0a, U1a, Ya, B, P);
-            primal(r + 1, X2b, U0b, U1b, Yb, P, A);
-        }
-        noise(t, std::integral_constant<int, 1>());
-        lds_barrier();
-    };
-    int t = T0;
-    for (; t + 2 < T1; t += 3) {
-        step(t, R0, R1, R2);
-        step(t + 1, R2, R0, R1);
-        step(t + 2, R1, R2, R0);
-    }
-    if (t < T1) step(t, R0, R1, R2);
-    if (t + 1 < T1) step(t + 1, R2, R0, R1);
-    flush();
-}
-
-template <bool EXACT>
-__device__ __forceinline__ void pair_pass(const TvArgs& a, PairShared& sh, const RowMap& rm, const int n,
-                                          const bool track, const long long step, const bool fresh) {
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (scalar branches)
-    const int H = a.H, W = a.W, C = a.C;
-    const size_t HW = (size_t)H * W;
-    const size_t BE = (size_t)a.B * C * HW;
-    const int par_in = (int)(step & 1), par_out = (int)((step + 1) & 1);
-    const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int Q = rm.Q;
-    const int qc0 = rm.htop, qc1 = Q - rm.hbot;          // core stream rows
-    const int gj0 = CPL * lane;
-    const bool lane_ok = gj0 < W;
-    const int gjc = min(gj0, W - CPL);                    // load column (every lane in bounds)
-    // steps T0 .. T1-1: noise of pair p from step p-5, the front's data term of pair p in step p-1, the
-    // hand-over in W_p; the back takes rows (2t - 3n, 2t - 3n + 1) at step t and finishes their stores
-    // in W_{t+2}
-    const int T0 = PR_T0;
-    const int T1 = (qc1 - 2 + 3 * n + 1) / 2 + 3;
-    const int role = (w < SP_FRONT) ? 0 : (w < SP_FRONT + n ? 1 : (w < SP_FRONT + n + SP_BACK ? 2 : 3));
-    const int k_st = w - SP_FRONT + 1;
-    const bool trk = track && role == 1 && (k_st - 1) >= 2 && (k_st - 1) <= n - 2;
-    // (plane, plane row) of stream row q, q clamped into the stream
-    auto locate = [&](int q, int& pl, int& rr) __attribute__((always_inline)) {
-        RowCursor c;
-        cursor_init(rm, c, min(max(q, 0), Q - 1));
-        pl = c.p;
-        rr = c.r;
-    };
-
-    if (role == 0) {
-        // ---------------- FRONT: pairs p = f, f + 4, ... ----------------
-        // With phs = (t - f) & 3 and p = t + 4 - phs, step t of front wave f does
-        //   phs 0  W: hand pair t to stage 1 (ring 0, Y ring); DMA piece B of pair p;  C: DMA piece C of pair p
-        //   phs 3  W: pair p's loads landed, data term of row a;  C: data term of row b, DMA piece A of pair p + 4
-        // (pieces: A = row a's X, y, u2 lo; B = row a's u2 hi, mask and row b's X; C = row b's y, u2, mask:
-        // each issued once its staging slot has been read, 2.5 - 3 steps before the data term).
-        const int f = w;
-        const float* xin = a.x[par_in];
-        const float* u2in = a.u2[par_in];
-        // LDS-DMA of part `part` (0 X, 1 y, 2 u2 lo, 3 u2 hi, 4 mask) of stream row q into staging slot i
-        auto dma = [&](int q, int i, int part) __attribute__((always_inline)) {
-            int pl, rr;
-            locate(q, pl, rr);
-            const int bb = pl / C;
-            const size_t base = (size_t)pl * HW + (size_t)rr * W + gjc;
-            if (part == 0) glds16(xin + base, &sh.fst[f][i][0][0]);
-            else if (part == 1)
-                glds16(a.yobs + (size_t)bb * a.y_cs + (size_t)(pl - bb * C) * HW + (size_t)rr * W + gjc,
-                       &sh.fst[f][i][1][0]);
-            else if (part == 2) glds16(u2in + 2 * base, &sh.fst[f][i][2][0]);
-            else if (part == 3) glds16(u2in + 2 * base + 4, &sh.fst[f][i][3][0]);
-            else glds4(a.mask + (size_t)bb * a.m_cs + (size_t)rr * W + gjc, &sh.fmk[f][i][0]);
-        };
-        float4 oY[2], oX[2], oU0[2], oU1[2];               // pair p's ring-0 rows, handed over in W_p
-        for (int i = 0; i < 2; ++i) oY[i] = oX[i] = oU0[i] = oU1[i] = zero4;
-        auto data_term = [&](int p, int i) __attribute__((always_inline)) {
-            const float4 fX = sh.fst[f][i][0][lane];
-            const float4 fYo = sh.fst[f][i][1][lane];
-            const float4 fU0 = sh.fst[f][i][2][lane];
-            const float4 fU1 = sh.fst[f][i][3][lane];
-            const uint32_t fMw = sh.fmk[f][i][lane];
-            const float4 fZ = sh.z[p & (PR_ZRING - 1)][i][lane];
-            const float X[CPL] = {fX.x, fX.y, fX.z, fX.w};
-            const float yo[CPL] = {fYo.x, fYo.y, fYo.z, fYo.w};
-            const float zn[CPL] = {fZ.x, fZ.y, fZ.z, fZ.w};
-            const float mk[CPL] = {(float)(fMw & 0xFFu), (float)((fMw >> 8) & 0xFFu),
-                                   (float)((fMw >> 16) & 0xFFu), (float)(fMw >> 24)};
-            float Yv[CPL];
-#pragma unroll
-            for (int kk = 0; kk < CPL; ++kk) {
-                if (EXACT) {
-                    const float g = (-mk[kk] * (X[kk] - yo[kk])) / a.sigma2;
-                    Yv[kk] = lane_ok ? (X[kk] + a.c1 * g) + a.c2 * zn[kk] : 0.f;
-                } else {
-                    const float g = (mk[kk] * (yo[kk] - X[kk])) * a.inv_sigma2;
-                    Yv[kk] = lane_ok ? __builtin_fmaf(a.c2, zn[kk], __builtin_fmaf(a.c1, g, X[kk])) : 0.f;
-                }
-            }
-            // component-wise selects: a select of whole float4 objects becomes a select of their addresses
-            // (scratch memory)
-            oY[i] = make_float4(Yv[0], Yv[1], Yv[2], Yv[3]);
-            float xs[CPL];
-#pragma unroll
-            for (int kk = 0; kk < CPL; ++kk) xs[kk] = lane_ok ? (fresh ? Yv[kk] : X[kk]) : 0.f;
-            oX[i] = make_float4(xs[0], xs[1], xs[2], xs[3]);
-            const float uk = fresh ? 0.f : 1.f;     // (u2 of a fresh TV start is 0; the loaded values are finite)
-            oU0[i] = fresh ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(fU0.x, fU0.z, fU1.x, fU1.z);
-            oU1[i] = fresh ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(fU0.y, fU0.w, fU1.y, fU1.w);
-            (void)uk;
-        };
-        for (int t = T0; t < T1; ++t) {
-            const int phs = (t - f) & 3;
-            const int p = t + 4 - phs;
-            const bool live = p >= 0 && 2 * p < Q;
-            // ---- W-phase
-            if (phs == 0) {
-                if (t >= 0 && 2 * t < Q) {                   // hand pair t to stage 1
-#pragma unroll
-                    for (int i = 0; i < 2; ++i) {
-                        sh.x2[0][i][lane] = oX[i];
-                        sh.u0[0][i][lane] = oU0[i];
-                        sh.u1[0][i][lane] = oU1[i];
-                        sh.y[pr_yslot(2 * t + i)][lane] = oY[i];
-                    }
-                }
-                if (live) { dma(2 * p, 0, 3); dma(2 * p, 0, 4); dma(2 * p + 1, 1, 0); }
-            } else if (phs == 3 && live) {
-                wait_vm0();                                   // pair p's loads landed
-                data_term(p, 0);
-            }
-            lds_barrier();
-            // ---- C-phase
-            if (phs == 0) {
-                if (live) { dma(2 * p + 1, 1, 1); dma(2 * p + 1, 1, 2); dma(2 * p + 1, 1, 3); dma(2 * p + 1, 1, 4); }
-            } else if (phs == 3) {
-                if (live) data_term(p, 1);
-                // row a's staging was read in this step's W-phase (drained by the barrier)
-                if (p + 4 >= 0 && 2 * (p + 4) < Q) { dma(2 * p + 8, 0, 0); dma(2 * p + 8, 0, 1); dma(2 * p + 8, 0, 2); }
-            }
-            lds_barrier();
-        }
-    } else if (role == 1) {
-        // ---------------- STAGE k_st (one inner TV iteration per wave; stages 1..3 also the noise) ----------------
-        __builtin_amdgcn_s_setprio(1);
-        const int lastk = W - 1 - gj0;                     // in 0..3 on the lane holding column W-1
-        if (trk) pair_stage<EXACT, true>(a, sh, rm, k_st, T0, T1, lane, lastk, lane_ok, step);
-        else pair_stage<EXACT, false>(a, sh, rm, k_st, T0, T1, lane, lastk, lane_ok, step);
-    } else if (role == 3) {
-        for (int t = T0; t < T1; ++t) { lds_barrier(); lds_barrier(); }
-    } else {
-        // ---------------- BACK: steps t = bw (mod 2), rows (2t - 3n, 2t - 3n + 1) of ring n ----------------
-        // Per pair (4 half-steps): C_t ring n + staging reads, accumulators, X stores, mean / sq DMA of row a
-        // of the pair of step t + 4; W_{t+1} u2 stores; C_{t+1} its row b DMA, row a's accumulator / sample
-        // stores; W_{t+2} row b's.
-        const int bw = w - SP_FRONT - n;
-        __builtin_amdgcn_s_setprio(3);
-        const StepInfo si = step_info(a, step, a.mean[par_out]);
-        const float* mean_in = a.mean[par_in];
-        const float* sq_in = a.sq[par_in];
-        const bool need_prev = si.acc && !si.first;
-        const int Qb = qc1;                                 // rows past the core end are never stored
-        auto row0 = [&](int t) __attribute__((always_inline)) { return 2 * t - 3 * n; };
-        auto stored = [&](int q) __attribute__((always_inline)) { return q >= qc0 && q < Qb; };
-        int nvm = 0;                                        // vector-memory ops issued by this wave
-        int mark0 = 0, mark1 = 0;                           // nvm after the mean / sq DMA into buffer 0 / 1
-        auto dma_row = [&](int t, int i) __attribute__((always_inline)) {                  // mean / sq of row i of the pair of step t
-            const int bi = ((t - bw) >> 1) & 1;
-            const int q = row0(t) + i;
-            if (need_prev && stored(q)) {
-                int pl, rr;
-                locate(q, pl, rr);
-                const size_t base = (size_t)pl * HW + (size_t)rr * W + gjc;
-                glds16(mean_in + base, &sh.bst[bw][bi][i][0][0]);
-                glds16(sq_in + base, &sh.bst[bw][bi][i][1][0]);
-                nvm += 2;
-            }
-            if (i == 1) { if (bi) mark1 = nvm; else mark0 = nvm; }
-        };
-        const int tb0 = T0 + ((bw - T0) & 1);
-        dma_row(tb0, 0); dma_row(tb0, 1);
-        dma_row(tb0 + 2, 0); dma_row(tb0 + 2, 1);
-        const int nheld = ((si.acc && (si.blockend || si.liveout)) ? 2 : 0) + (si.sample ? 1 : 0);
-        bool ok[2] = {false, false};                        // the pair's rows that are stored
-        size_t hb[2] = {0, 0};
-        float4 hU0[2], hU1[2], hM[2], hQ[2], hX[2];
-        for (int i = 0; i < 2; ++i) hU0[i] = hU1[i] = hM[i] = hQ[i] = hX[i] = zero4;
-        auto held = [&](int i) __attribute__((always_inline)) {                            // accumulator / block-mean / sample stores of row i
-            if (!ok[i]) return;
-            if (lane_ok) {
-                if (si.acc) {
-                    if (si.blockend) {
-                        st_nt(a.blocks + (size_t)si.blk * BE + hb[i], hM[i]);
-                        st_nt(a.blocks2 + (size_t)si.blk * BE + hb[i], hQ[i]);
-                    } else if (si.liveout) {
-                        st_nt(a.mean[par_out] + hb[i], hM[i]);
-                        st_nt(a.sq[par_out] + hb[i], hQ[i]);
-                    }
-                }
-                if (si.sample) st_nt(a.samples + (size_t)si.sidx * BE + hb[i], hX[i]);
-            }
-            nvm += nheld;
-        };
-        for (int t = T0; t < T1; ++t) {
-            const bool mine = ((t - bw) & 1) == 0;          // C_t takes a pair
-            // ---- W-phase
-            if (!mine) {                                    // W_{t'+1} of the pair taken at t' = t - 1
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    if (!ok[i]) continue;
-                    if (lane_ok) {
-                        float* u2o = a.u2[par_out] + 2 * hb[i];
-                        st_nt(u2o, make_float4(hU0[i].x, hU1[i].x, hU0[i].y, hU1[i].y));
-                        st_nt(u2o + 4, make_float4(hU0[i].z, hU1[i].z, hU0[i].w, hU1[i].w));
-                    }
-                    nvm += 2;
-                }
-            } else {
-                held(1);                                    // W_{t'+2} of the pair taken at t' = t - 2
-                ok[1] = false;
-            }
-            lds_barrier();
-            // ---- C-phase
-            if (mine) {
-                const int c = row0(t);
-                const int bi = ((t - bw) >> 1) & 1;
-                ok[0] = stored(c);
-                ok[1] = stored(c + 1);
-                if (ok[0] || ok[1]) {
-                    if (si.acc && need_prev) wait_vm_n(nvm - (bi ? mark1 : mark0));   // this pair's mean / sq
-#pragma unroll
-                    for (int i = 0; i < 2; ++i) {
-                        const float4 X2 = sh.x2[n][i][lane];
-                        hU0[i] = sh.u0[n][i][lane];
-                        hU1[i] = sh.u1[n][i][lane];
-                        hX[i] = X2;
-                        hM[i] = hQ[i] = zero4;
-                        if (si.acc) {
-                            float4 bm = zero4, bq = zero4;
-                            if (need_prev) {
-                                bm = sh.bst[bw][bi][i][0][lane];
-                                bq = sh.bst[bw][bi][i][1][lane];
-                            }
-                            const float xs[CPL] = {X2.x, X2.y, X2.z, X2.w};
-                            const float ms[CPL] = {bm.x, bm.y, bm.z, bm.w};
-                            const float qs[CPL] = {bq.x, bq.y, bq.z, bq.w};
-                            float m[CPL], qq[CPL];
-#pragma unroll
-                            for (int kk = 0; kk < CPL; ++kk) {
-                                if (si.first) {
-                                    m[kk] = si.cb * xs[kk];
-                                    qq[kk] = si.cb * (xs[kk] * xs[kk]);
-                                } else {
-                                    m[kk] = si.ca * ms[kk] + si.cb * xs[kk];
-                                    qq[kk] = si.ca * qs[kk] + si.cb * (xs[kk] * xs[kk]);
-                                }
-                            }
-                            hM[i] = make_float4(m[0], m[1], m[2], m[3]);
-                            hQ[i] = make_float4(qq[0], qq[1], qq[2], qq[3]);
-                        }
-                    }
-                    // every staging read returned before the buffer is re-targeted (pair of step t + 4)
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-                    for (int i = 0; i < 2; ++i) {
-                        if (!ok[i]) continue;
-                        int pl, rr;
-                        locate(c + i, pl, rr);
-                        hb[i] = (size_t)pl * HW + (size_t)rr * W + gj0;
-                        if (lane_ok) st_nt(a.x[par_out] + hb[i], hX[i]);
-                        nvm += 1;
-                    }
-                }
-                dma_row(t + 4, 0);
-            } else {                                        // C_{t'+1} of the pair taken at t' = t - 1
-                dma_row(t + 3, 1);
-                held(0);
-                ok[0] = false;
-            }
-            lds_barrier();
-        }
-    }
-}
-
-template <bool EXACT>
-__global__ void __launch_bounds__(TV_THREADS) tv_pair_kernel(const TvArgs a) {
-    __shared__ PairShared sh;
-    __shared__ int s_stop[MAXG];
-    __shared__ int s_flag, s_item, s_next;
-    const int C = a.C;
-    const long long step = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
-    const bool fresh = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
-    {
-        RowMap rm;
-        build_rowmap(a, blockIdx.x, rm);
-        pair_pass<EXACT>(a, sh, rm, a.n_tv, true, step, fresh);
-        if (!a.fin_inline) return;        // main-pass-only launch (kernel timing): no side effects
-        // rel_err partial sums of this stream -> global, per segment's chain (deepinv's early-stop
-        // test, per chain); the tracking stages wrote sh.red[segment][k - 1]
-        lds_barrier();
-        for (int tt = threadIdx.x; tt < SP_MAXSEG * SP_MAXST; tt += blockDim.x) {
-            const int sg = tt / SP_MAXST, it = tt - sg * SP_MAXST;     // it = k - 1
-            if (sg < rm.ns && it >= 2 && it <= a.n_tv - 2) {
-                const int g = a.per_chain_norm ? rm.pl(sg) / C : 0;
-                atomicAdd(&a.norms[((size_t)g * a.n_tv + it) * 2], (double)sh.red[sg][it][0]);
-                atomicAdd(&a.norms[((size_t)g * a.n_tv + it) * 2 + 1], (double)sh.red[sg][it][1]);
-            }
-        }
-    }
-    // ---- step finalisation by the last workgroup to arrive (as tv_stream_kernel) ----
-    wait_vm0();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const int old = __hip_atomic_fetch_add(a.arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_flag = (old == (int)gridDim.x - 1) ? 1 : 0;
-        if (s_flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    wait_vm0();
-    __syncthreads();
-    if (!s_flag) return;
-    const int G = a.B;
-    for (int g = threadIdx.x; g < G; g += blockDim.x) s_stop[g] = 0;
-    __syncthreads();
-    for (int i = threadIdx.x; i < G * SP_MAXST; i += blockDim.x) {
-        const int g = i / SP_MAXST, t = i - g * SP_MAXST;
-        if (t >= 2 && t <= a.n_tv - 2) {
-            const double nd = a.norms[((size_t)g * a.n_tv + t) * 2];
-            const double nn = a.norms[((size_t)g * a.n_tv + t) * 2 + 1];
-            const float rel = (float)sqrt(nd) / (float)sqrt(nn);
-            if (rel < a.tol) atomicOr(&s_stop[g], 1 << t);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) { s_next = 0; s_item = 0; }
-    __syncthreads();
-    for (int g = threadIdx.x; g < G; g += blockDim.x) {
-        const int m = s_stop[g];
-        s_stop[g] = m ? (__ffs(m) - 1) + 1 : a.n_tv;
-        if (m) s_item = 1;
-    }
-    __syncthreads();
-    if (s_item == 0) s_next = 1 << 30;        // common case: nothing to redo
-    // rare: re-stream every plane of a stopped chain with the stopped iteration count (the step's
-    // inputs are intact: ping-pong state)
-    for (;;) {
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const int items = a.B * C;
-            int it = min(s_next, items), found = -1;
-            for (; it < items; ++it)
-                if (s_stop[it / C] < a.n_tv) { found = it; break; }
-            s_item = found;
-            s_next = it + 1;
-        }
-        __syncthreads();
-        const int item = __builtin_amdgcn_readfirstlane(s_item);
-        if (item < 0) break;
-        RowMap rm;
-        plane_rowmap(a.H, item, rm);
-        const int nstop = __builtin_amdgcn_readfirstlane(s_stop[item / C]);
-        pair_pass<EXACT>(a, sh, rm, nstop, false, step, fresh);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < a.B * a.n_tv * 2; i += blockDim.x) a.norms[i] = 0.0;
-    if (threadIdx.x == 0) {
-        *a.arrive = 0;
-        if (a.fresh_dev) *a.fresh_dev = 0;
-        if (a.advance_step && a.d_step) *a.d_step = *a.d_step + 1;
     }
 }
 
@@ -3430,13 +2905,6 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
             s.fin_inline = (mask & 2) ? 1 : 0;
             const int grid = s.split_wgs > 0 ? s.split_wgs : P * s.st_nsegs;   // virtual planes
             const bool gen = !(s.ldw == s.W && s.st_nsegs == 1);
-            if constexpr (ALPHA1) {
-                if (s.pair) {
-                    if (gen) return fail(0, "psgla_tv_step: row-pair kernel on a padded / segmented shape");
-                    hipLaunchKernelGGL((tv_pair_kernel<EXACT>), dim3(grid), dim3(TV_THREADS), 0, st, s);
-                    return launch_check("tv_pair_kernel");
-                }
-            }
             if (!gen)
                 hipLaunchKernelGGL((tv_stream_kernel<EXACT, ALPHA1, false>), dim3(grid), dim3(TV_THREADS), 0, st, s);
             else
@@ -3479,15 +2947,10 @@ static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
     const bool streamable = (a.ldw % 4 == 0) && d->n_tv >= 1 && d->n_tv <= SP_MAXST && d->H >= 2 &&
                             stream_segments(a.W, a.ldw, d->n_tv, nullptr) > 0;
     a.stream = streamable && d->kernel_variant != 1;
-    if ((d->kernel_variant == 2 || d->kernel_variant == 3) && !streamable)
+    if (d->kernel_variant == 2 && !streamable)
         { g_sel_err = "psgla_tv_step: shape not supported by the streaming kernel"; return -1; }
-    if (d->kernel_variant < 0 || d->kernel_variant > 4)
-        { g_sel_err = "psgla_tv_step: kernel_variant outside 0..4"; return -1; }
-    // row-pair pipeline: one 256-column window (W <= 256, W % 4 == 0, no row padding), alpha == 1
-    const bool pairable = streamable && a.ldw == a.W && a.W <= TV_COLS && d->x2[0] == nullptr && d->n_tv >= PR_NZ;
-    if (d->kernel_variant == 3 && !pairable)
-        { g_sel_err = "psgla_tv_step: shape not supported by the row-pair kernel (W <= 256, W % 4 == 0, alpha == 1, n_tv >= 3)"; return -1; }
-    a.pair = pairable && d->kernel_variant == 3 ? 1 : 0;     // forced only: measured slower
+    if (d->kernel_variant < 0 || d->kernel_variant > 4 || d->kernel_variant == 3)
+        { g_sel_err = "psgla_tv_step: kernel_variant must be 0 (auto), 1 (band), 2 (stream) or 4 (tile)"; return -1; }
     // small-batch tile kernel: forced (variant 4) or, in auto mode, when all tiles fit in one round
     // on the CUs (a row stream would be mostly pipeline fill: strong scaling's 64/N chains per GPU)
     a.tile_r = 0;
@@ -3503,7 +2966,6 @@ static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
             a.nsegs = 1;
             a.tiles = nb;
             a.stream = 0;
-            a.pair = 0;
         }
     }
     if (!a.stream && a.tile_r == 0 && a.ldw != a.W) { g_sel_err = "psgla_tv_step: a row pitch ldw != W needs the streaming kernel"; return -1; }
@@ -3518,7 +2980,7 @@ static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
         }
     }
     if (a.tile_r > 0) return 3;
-    if (a.stream) return a.pair ? 2 : 1;
+    if (a.stream) return 1;
     return 0;
 }
 

@@ -176,14 +176,14 @@ class DRUNet(torch.nn.Module):
         return self._forward_dispatch(x).contiguous()
 
     def _forward_dispatch(self, x):
-        """deepinv 0.2.1 DRUNet.forward's size dispatch (KAIR utils_model): the U-Net itself when both
-        sides are multiples of 8 and > 31 (or in training mode); replicate padding to multiples of 16
-        (test_pad) when a side is < 32; otherwise four overlapping quadrants cut on a 64-pixel grid
+        """deepinv 0.2.1 DRUNet.forward's size dispatch (KAIR utils_model): the U-Net itself in eval mode
+        when both sides are multiples of 8 and > 31; replicate padding to multiples of 16 (test_pad) in
+        training mode or when a side is < 32; otherwise four overlapping quadrants cut on a 64-pixel grid
         (test_onesplit, refield 64), each run alone, stitched back."""
         h, w = x.size(2), x.size(3)
-        if self.training or (h % 8 == 0 and w % 8 == 0 and h > 31 and w > 31):
+        if not self.training and h % 8 == 0 and w % 8 == 0 and h > 31 and w > 31:
             return self.forward_unet(x)
-        if h < 32 or w < 32:
+        if self.training or h < 32 or w < 32:
             return _test_pad(self.forward_unet, x, modulo=16)
         return _test_onesplit(self.forward_unet, x, refield=64)
 

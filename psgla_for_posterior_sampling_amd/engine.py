@@ -20,7 +20,7 @@ from . import hip_ops as K
 
 
 # PsglaTvStep.kernel_variant (include/psgla_hip.h)
-KERNEL_VARIANTS = {"auto": 0, "band": 1, "stream": 2, "pair": 3, "tile": 4}
+KERNEL_VARIANTS = {"auto": 0, "band": 1, "stream": 2, "tile": 4}
 
 
 class FusedTvChains:
@@ -43,7 +43,7 @@ class FusedTvChains:
         # of the first W columns
         if kernel_variant not in KERNEL_VARIANTS:
             raise ValueError(f"kernel_variant must be one of {sorted(KERNEL_VARIANTS)}")
-        self.ldw = Wd if (Wd % 4 == 0 or kernel_variant in ("band", "tile", "pair")) else (Wd + 3) // 4 * 4
+        self.ldw = Wd if (Wd % 4 == 0 or kernel_variant in ("band", "tile")) else (Wd + 3) // 4 * 4
         self.pshape = (B, C, H, self.ldw)
         self.device = dev
         self.alpha = float(alpha)
@@ -198,13 +198,12 @@ class FusedTvChains:
     def main_kernel(self) -> str:
         """Name of the kernel psgla_tv_step dispatches for this shape (the library's own choice,
         psgla_tv_step_kernel: the small-batch tile kernel when its tiles fit on the CUs at once, else
-        the row-pair pipeline for unpadded rows of <= 256 columns at alpha == 1, else the row stream
-        (W % 4 == 0 rows -- always, the engine pads rows --, 1 <= n_tv <= 10, H >= 2); the band
+        the row stream (W % 4 == 0 rows -- always, the engine pads rows --, 1 <= n_tv <= 10, H >= 2); the band
         kernel otherwise or when forced)."""
         k = N.lib().psgla_tv_step_kernel(ctypes.byref(self.desc))
         if k < 0:
             raise RuntimeError(N.lib().psgla_last_error().decode())
-        return ("tv_main_kernel", "tv_stream_kernel", "tv_pair_kernel", "tv_tile_kernel")[k]
+        return {0: "tv_main_kernel", 1: "tv_stream_kernel", 3: "tv_tile_kernel"}[k]
 
     def launch_main_only(self, n: int = 1):
         """Launch only the fused tile kernel n times for the CURRENT step (idempotent: it reads

@@ -44,8 +44,8 @@ def test_denoiser_prior_matches_reference_closure():
 
 
 def test_drunet_size_dispatch_follows_deepinv():
-    """deepinv 0.2.1 DRUNet.forward's routes (KAIR utils_model): forward_unet for sides % 8 == 0 and
-    > 31, test_pad(modulo 16) when a side is < 32, test_onesplit(refield 64) otherwise.  With an
+    """deepinv 0.2.1 DRUNet.forward's routes (KAIR utils_model): forward_unet in eval mode for sides
+    % 8 == 0 and > 31, test_pad in training mode or(modulo 16) when a side is < 32, test_onesplit(refield 64) otherwise.  With an
     elementwise stand-in for the U-Net every route returns exactly 2 x its input (the stitching is
     checked pixel for pixel); the recorded input shapes name the route."""
     m = DRUNet(nc=(8, 16, 32, 64), nb=1)
@@ -66,6 +66,14 @@ def test_drunet_size_dispatch_follows_deepinv():
             x = torch.rand(1, 3, h, w)
             y = m(x, 0.05)
             assert seen == shapes, (h, w, seen)
+            assert torch.equal(y, 2 * x), (h, w)
+        # training mode: test_pad(modulo 16) at every size (deepinv takes forward_unet only in eval mode)
+        m.train()
+        for (h, w), shape in [((64, 40), (64, 48)), ((100, 72), (112, 80)), ((64, 64), (64, 64))]:
+            seen.clear()
+            x = torch.rand(1, 3, h, w)
+            y = m(x, 0.05)
+            assert seen == [shape], (h, w, seen)
             assert torch.equal(y, 2 * x), (h, w)
 
 

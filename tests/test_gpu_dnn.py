@@ -3,6 +3,8 @@
 the step-by-step generic loop (same kernels, same denoiser: bit for bit), and against the CPU
 oracle (restoration_algorithms.py restated) within the north-star tolerance -- the convolutions
 run in MIOpen on the GPU and in ATen on the CPU, so the denoiser itself is not bit-identical."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -305,6 +307,55 @@ def test_save_images_online_keeps_the_fast_path(tmp_path, den_kind):
     assert len(d["Samples"]) == i_last // 3 + 1          # samples at i % n_inter == 0, i <= i_last
     assert len(d["Mmse"]) == (i_last + 1) // 5           # blocks of n_inter_mmse + 1 steps completed
     assert d["n_iter"] == n
+
+
+@pytest.mark.parametrize("exact", [True, False])
+def test_save_images_online_y_matches_oracle(tmp_path, exact):
+    """The y_i.png image of the fused TV path (restoration_algorithms.py:246-253: Y of step i, the input of
+    the prox) is rebuilt after the step from X_i by the standalone inpaint_grad + langevin_update kernels;
+    it equals the oracle's Y at step i (the tensor its psgla hands to denoiser.forward) bit for bit when the
+    kernels run in exact mode, within the 1e-5 relative north-star tolerance in fast mode (the rebuild reads the fast chain's X_i)."""
+    from psgla_for_posterior_sampling_amd import restoration_algorithms as RA
+    from psgla_for_posterior_sampling_amd.denoisers import TVDenoiser
+    from psgla_for_posterior_sampling_amd.fidelity import InpaintingFidelity
+    g = torch.Generator().manual_seed(2)
+    x = torch.rand((1, 3, 24, 40), generator=g)
+    dg_ref, y, init, mask2d = orc.inpainting_problem(x, seed_ip=0)
+    dg = InpaintingFidelity(mask2d.to(DEV), y.to(DEV), torch.tensor((1 / 255.0) ** 2, dtype=torch.float32))
+    s, lam, n = 10 / 255.0, 10.0, 30
+    kw = dict(sig_float=s, delta=s ** 2, n_iter=n, n_inter=3, n_inter_mmse=4, seed=4)
+
+    class RecordingTV(orc.TVDenoiser):
+        def __init__(self):
+            super().__init__(n_it_max=10)
+            self.ys = []
+
+        def forward(self, y_in, ths=None):
+            self.ys.append(y_in.clone())
+            return super().forward(y_in, ths)
+    tv = RecordingTV()
+    orc.psgla(init, dg_ref, tv, torch.tensor(1.0), torch.tensor(lam), chain=0, **kw)
+
+    seen = {}
+    orig = RA._Snapshots.save
+
+    def save(self, i, X, Y, lists):
+        seen[i] = Y.detach().cpu().clone()
+        return orig(self, i, X, Y, lists)
+    RA._Snapshots.save = save
+    try:
+        RA.psgla(init.to(DEV), dg, TVDenoiser(n_it_max=10, exact=exact), torch.tensor(1.0), torch.tensor(lam),
+                 path=str(tmp_path), save_images_online=True, name="nm", graph_steps=4, **kw)
+    finally:
+        RA._Snapshots.save = orig
+    assert sorted(seen) == list(range(0, n, n // 10))
+    for i, Yi in seen.items():
+        if exact:
+            assert torch.equal(Yi, tv.ys[i]), i
+        else:
+            d = float(torch.linalg.vector_norm((Yi - tv.ys[i]).double()) / torch.linalg.vector_norm(tv.ys[i].double()))
+            assert d < REL_TOL_MEAN, (i, d)
+        assert os.path.exists(os.path.join(str(tmp_path), f"y_{i}.png"))
 
 
 def test_tv_prox_long_n_it_chunked_vs_oracle():

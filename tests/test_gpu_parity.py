@@ -173,7 +173,8 @@ def test_fused_psgla_tv_fast_within_tolerance():
     assert Xl.shape == fx["samples"].shape
 
 
-def _fused_batch(B, chain0, exact, n_iter=40, H=48, W=64, alpha=1.0, variant="auto", stream_wgs=0):
+def _fused_batch(B, chain0, exact, n_iter=40, H=48, W=64, alpha=1.0, variant="auto", stream_wgs=0, n_inter=5,
+                 n_inter_mmse=4):
     from psgla_for_posterior_sampling_amd.engine import FusedTvChains
     from psgla_for_posterior_sampling_amd import hip_ops as K
     g = torch.Generator().manual_seed(5)
@@ -183,12 +184,12 @@ def _fused_batch(B, chain0, exact, n_iter=40, H=48, W=64, alpha=1.0, variant="au
     eng = FusedTvChains(init.expand(B, -1, -1, -1).contiguous().to(DEV), y.to(DEV),
                         mask2d.to(torch.uint8).to(DEV), c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
                         alpha=alpha, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10), seed=3,
-                        n_iter=n_iter, n_inter=5, n_inter_mmse=4, chain0=chain0, exact=exact,
+                        n_iter=n_iter, n_inter=n_inter, n_inter_mmse=n_inter_mmse, chain0=chain0, exact=exact,
                         kernel_variant=variant, stream_wgs=stream_wgs)
     return eng, (dg, y, init, mask2d, c1, c2)
 
 
-@pytest.mark.parametrize("variant", ["stream", "pair", "band"])
+@pytest.mark.parametrize("variant", ["stream", "band", "tile"])
 def test_fused_chains_independent_of_batching_and_graph(variant):
     """Chain k's trajectory depends only on (seed, global chain id): B=4 batch vs B=2 batch
     with chain0=2, and eager vs hipGraph replay -- bit-identical (multi-GPU sharding property)."""
@@ -205,8 +206,7 @@ def test_fused_chains_independent_of_batching_and_graph(variant):
 
 
 @pytest.mark.parametrize("variant,H,W", [("stream", 48, 64), ("band", 48, 64), ("stream", 70, 300),
-                                          ("band", 70, 300), ("auto", 37, 29), ("pair", 48, 64), ("pair", 37, 28),
-                                          ("pair", 21, 256)])
+                                          ("band", 70, 300), ("auto", 37, 29)])
 def test_fused_multichain_exact_vs_oracle(variant, H, W):
     B = 3
     eng, (dg, y, init, mask2d, c1, c2) = _fused_batch(B, 10, exact=True, n_iter=30, H=H, W=W, variant=variant)
@@ -238,16 +238,15 @@ def _oracle_chain(init, dg, n_iter, chain):
     return _ORACLE_CACHE[key]
 
 
-@pytest.mark.parametrize("variant", ["stream", "pair"])
+@pytest.mark.parametrize("variant", ["stream"])
 @pytest.mark.parametrize("stream_wgs", [-1, 3, 4, 7, 11, 20, 97])
 def test_stream_row_split_exact_vs_oracle(stream_wgs, variant):
     """Row-split streaming (the plane rows of all chains cut into stream_wgs ranges, n_tv halo rows
-    at cuts inside a plane, ranges spanning plane boundaries, odd row counts for the row-pair
-    pipeline): bit-identical to the checker for every cut position; -1 = one workgroup per plane."""
+    at cuts inside a plane, ranges spanning plane boundaries): bit-identical to the checker for every cut position; -1 = one workgroup per plane."""
     B, H, W, n_iter = 3, 48, 64, 20
     eng, (dg, y, init, mask2d, c1, c2) = _fused_batch(B, 10, exact=True, n_iter=n_iter, H=H, W=W,
                                                       variant=variant, stream_wgs=stream_wgs)
-    assert eng.main_kernel == ("tv_pair_kernel" if variant == "pair" else "tv_stream_kernel")
+    assert eng.main_kernel == "tv_stream_kernel"
     eng.run(n_iter, graph_steps=0)
     torch.cuda.synchronize()
     bm, bm2 = eng.blocks()
@@ -270,7 +269,7 @@ class _RecordingTV(orc.TVDenoiser):
         return out
 
 
-@pytest.mark.parametrize("variant", ["stream", "pair"])
+@pytest.mark.parametrize("variant", ["stream"])
 @pytest.mark.parametrize("stream_wgs", [0, -1])
 def test_stream_early_stop_exact_vs_oracle(stream_wgs, variant):
     """tol large enough that deepinv's early stop fires in some steps: the stream kernel's last
@@ -334,7 +333,7 @@ def test_fused_full_size_fast_vs_exact():
     dg, y, init, mask2d, _ = inpainting_problem(x)
     c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
     outs = []
-    for exact, variant in ((True, "stream"), (False, "stream"), (True, "band"), (True, "pair"), (False, "pair")):
+    for exact, variant in ((True, "stream"), (False, "stream"), (True, "band")):
         eng = FusedTvChains(init.expand(64, -1, -1, -1).contiguous(), y, dg.mask_u8, c1=c1, c2=c2,
                             sigma2=dg.sigma2, alpha=1.0, ths=float(np.float32(10 / 255.0)),
                             tv=K.TvConstants(n_it_max=10), seed=0, n_iter=12, n_inter=10, n_inter_mmse=10,
@@ -342,57 +341,99 @@ def test_fused_full_size_fast_vs_exact():
         eng.run(12, graph_steps=0)
         torch.cuda.synchronize()
         outs.append((eng.X.clone(), eng.blocks()[0].clone()))
-    (xe, be), (xf, bf), (xb, bb), (xpe, bpe), (xpf, bpf) = outs
+    (xe, be), (xf, bf), (xb, bb) = outs
     assert torch.equal(xe, xb) and torch.equal(be, bb)      # the exact kernels agree bit for bit
-    assert torch.equal(xe, xpe) and torch.equal(be, bpe)
-    assert torch.equal(xf, xpf) and torch.equal(bf, bpf)    # fast: the same per-element arithmetic
     assert torch.isfinite(xf).all() and torch.isfinite(xe).all()
     assert rel(bf.cpu().numpy(), be.cpu().numpy()) < REL_TOL_MEAN
     assert rel(xf.cpu().numpy(), xe.cpu().numpy()) < 1e-4
 
 
-def test_fused_full_size_fast_vs_exact_config1_length():
-    """The benched (fast) kernel over BASELINE configs[1]'s whole chain length: 64 chains x
-    3x256x256, N = 10000 PSGLA+TV(10) steps, graph-replayed in 100-step segments, the fast and the
-    exact tv_stream_kernel side by side on identical inputs.  The exact kernel is bit-identical to
-    the CPU oracle (tests above), so this bounds fast-vs-oracle on the sample mean by transitivity:
-    the mean of the block means (the MMSE the reference reports, sampling_images.py:428) and of the
-    second-moment blocks within the north-star 1e-5 relative, every block within 1e-5, and both
-    chains make the same early-stop decisions (same final TV state to fp32 noise)."""
+def _relt(a, b):
+    return float(torch.linalg.vector_norm((a - b).double()) / torch.linalg.vector_norm(b.double()))
+
+
+def test_fused_full_size_fast_vs_exact_config1_schedule():
+    """The benched (fast) kernel over BASELINE configs[1]'s whole run AT ITS REAL SCHEDULE: 64 chains x
+    3x256x256, N = 10000 PSGLA+TV(10) steps, n_inter = n_inter_mmse = 10 (sampling_images.py:105-106
+    with N = 10000: 1,000 stored samples and 909 blocks of 11 samples), graph-replayed in 100-step
+    segments, fast and exact kernels side by side on identical inputs.  The exact kernel is
+    bit-identical to the CPU oracle (tests above).  Asserted against exact mode: every block mean and
+    second-moment block, their means over blocks (the MMSE of sampling_images.py:428) within the
+    north-star 1e-5 relative, every stored sample within 1e-4 relative.  The 64 chains run as two
+    32-chain halves (chain0 = 0 / 32) so both modes' stores (71 GB each) fit in HBM together: a chain's
+    values do not depend on the batch it runs in (test_fused_chains_independent_of_batching_and_graph)."""
     from psgla_for_posterior_sampling_amd.engine import FusedTvChains
     from psgla_for_posterior_sampling_amd import hip_ops as K
-    B, n = 64, 10000
-    xs = torch.empty((B, 3, 256, 256), device=DEV)
-    for b in range(B):
-        xs[b] = torch.rand((3, 256, 256), generator=torch.Generator(device=DEV).manual_seed(1234 + b), device=DEV)
+    n, half = 10000, 32
     gen = torch.Generator(device=DEV).manual_seed(0)
     mask2d = (torch.rand((256, 256), generator=gen, device=DEV) > 0.5).to(torch.uint8)
     mask = mask2d.float()[None, None]
-    y = mask * xs + torch.normal(torch.zeros_like(xs), std=(1 / 255.0) * torch.ones_like(xs), generator=gen)
-    init = (mask * y + (1 - mask) * 0.5).contiguous()
     c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
-    res = {}
-    for exact in (True, False):
-        eng = FusedTvChains(init, y.contiguous(), mask2d, c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
-                            alpha=1.0, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10), seed=0,
-                            n_iter=n, n_inter=10, n_inter_mmse=1000, exact=exact, store_samples=False)
-        eng.run(n, graph_steps=100)
+    worst = {"block": 0.0, "block2": 0.0, "sample": 0.0}
+    for chain0 in (0, half):
+        xs = torch.empty((half, 3, 256, 256), device=DEV)
+        for b in range(half):
+            xs[b] = torch.rand((3, 256, 256), generator=torch.Generator(device=DEV).manual_seed(1234 + chain0 + b),
+                               device=DEV)
+        gy = torch.Generator(device=DEV).manual_seed(100 + chain0)
+        y = mask * xs + torch.normal(torch.zeros_like(xs), std=(1 / 255.0) * torch.ones_like(xs), generator=gy)
+        init = (mask * y + (1 - mask) * 0.5).contiguous()
+        engs = {}
+        for exact in (True, False):
+            eng = FusedTvChains(init, y.contiguous(), mask2d, c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
+                                alpha=1.0, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10), seed=0,
+                                n_iter=n, n_inter=10, n_inter_mmse=10, chain0=chain0, exact=exact)
+            assert eng.main_kernel == "tv_stream_kernel"
+            eng.run(n, graph_steps=100)
+            engs[exact] = eng
         torch.cuda.synchronize()
-        b1, b2 = eng.blocks()
-        res[exact] = (b1.clone(), b2.clone(), eng.X.clone())
-        del eng, b1, b2
+        (e1, e2), (f1, f2) = engs[True].blocks(), engs[False].blocks()
+        es, fs = engs[True].samples(), engs[False].samples()
+        assert e1.shape[0] == 909 and f1.shape[0] == 909 and es.shape[0] == 1000 and fs.shape[0] == 1000
+        assert torch.isfinite(f1).all() and torch.isfinite(fs).all()
+        assert _relt(f1.mean(0), e1.mean(0)) < REL_TOL_MEAN
+        assert _relt(f2.mean(0), e2.mean(0)) < REL_TOL_MEAN
+        for k in range(e1.shape[0]):
+            worst["block"] = max(worst["block"], _relt(f1[k], e1[k]))
+            worst["block2"] = max(worst["block2"], _relt(f2[k], e2[k]))
+        for k in range(es.shape[0]):
+            worst["sample"] = max(worst["sample"], _relt(fs[k], es[k]))
+        del engs, e1, e2, f1, f2, es, fs
         torch.cuda.empty_cache()
-    (e1, e2, ex), (f1, f2, fx_) = res[True], res[False]
-    assert e1.shape[0] == n // 1001 and torch.isfinite(f1).all() and torch.isfinite(fx_).all()
+    print("fast vs exact, config[1] schedule, worst relative:", worst)
+    assert worst["block"] < REL_TOL_MEAN and worst["block2"] < REL_TOL_MEAN
+    assert worst["sample"] < 1e-4
 
-    def relt(a, b):
-        return float(torch.linalg.vector_norm((a - b).double()) / torch.linalg.vector_norm(b.double()))
-    assert relt(f1.mean(0), e1.mean(0)) < REL_TOL_MEAN
-    assert relt(f2.mean(0), e2.mean(0)) < REL_TOL_MEAN
-    for k in range(e1.shape[0]):
-        assert relt(f1[k], e1[k]) < REL_TOL_MEAN, k
-        assert relt(f2[k], e2[k]) < REL_TOL_MEAN, k
-    assert relt(fx_, ex) < 1e-4
+
+@pytest.mark.parametrize("variant", ["stream", "tile"])
+def test_fused_fast_vs_oracle_direct_10000_steps(variant):
+    """Fast mode against the CPU oracle's psgla (oracle/psgla_oracle.py, the restatement of
+    restoration_algorithms.py:219-271) directly, not by transitivity: 1 chain x 3x24x40, N = 10000
+    steps at configs[1]'s schedule (n_inter = n_inter_mmse = 10).  Every block mean and second-moment
+    block and their means over blocks within 1e-5 relative, every stored sample within 1e-4."""
+    n = 10000
+    eng, (dg, y, init, mask2d, c1, c2) = _fused_batch(1, 0, exact=False, n_iter=n, H=24, W=40, variant=variant,
+                                                      n_inter=10, n_inter_mmse=10)
+    assert eng.main_kernel == "tv_" + variant + "_kernel"
+    eng.run(n, graph_steps=100)
+    torch.cuda.synchronize()
+    key = ("direct", n)
+    if key not in _ORACLE_CACHE:
+        tv = orc.TVDenoiser(n_it_max=10)
+        Xl, Ml, M2l = orc.psgla(init, dg, tv, torch.tensor(1.0), torch.tensor(10.0), sig_float=10 / 255.0,
+                                delta=(10 / 255.0) ** 2, n_iter=n, n_inter=10, n_inter_mmse=10, seed=3, chain=0)
+        _ORACLE_CACHE[key] = [torch.stack(v) for v in (Xl, Ml, M2l)]
+    Xs, Ms, M2s = _ORACLE_CACHE[key]
+    bm, bm2 = (t[:, 0].cpu() for t in eng.blocks())
+    sm = eng.samples()[:, 0].cpu()
+    assert bm.shape == Ms.shape and sm.shape == Xs.shape and bm.shape[0] == 909
+    assert _relt(bm.mean(0), Ms.mean(0)) < REL_TOL_MEAN
+    assert _relt(bm2.mean(0), M2s.mean(0)) < REL_TOL_MEAN
+    wb = max(_relt(bm[k], Ms[k]) for k in range(bm.shape[0]))
+    wb2 = max(_relt(bm2[k], M2s[k]) for k in range(bm.shape[0]))
+    ws = max(_relt(sm[k], Xs[k]) for k in range(sm.shape[0]))
+    print(f"fast {variant} vs oracle, 10000 steps, worst relative: block {wb:.3g} block2 {wb2:.3g} sample {ws:.3g}")
+    assert wb < REL_TOL_MEAN and wb2 < REL_TOL_MEAN and ws < 1e-4
 
 
 # ------------------------------------------------------------------------------ generic paths
@@ -691,43 +732,6 @@ def test_stream_segmented_early_stop_exact_vs_oracle():
         np.testing.assert_array_equal(eng.samples()[:, b].cpu().numpy(), np.stack([t.numpy() for t in Xl]))
         np.testing.assert_array_equal(eng.u2_state[b].cpu().numpy(), tv.u2.numpy()[0])
     assert fired, "test needs the early stop to fire"
-
-
-# ------------------------------------------------------------------------------ row-pair pipeline
-@pytest.mark.parametrize("exact,H,W,stream_wgs,tol,B,n_tv", [
-    (True, 48, 64, 0, 1e-5, 3, 10), (True, 48, 64, 7, 1e-5, 3, 10), (True, 48, 64, -1, 1e-5, 3, 10),
-    (False, 48, 64, 11, 1e-5, 3, 10), (True, 37, 28, 5, 1e-5, 3, 10), (True, 40, 52, 0, 3e-2, 2, 10),
-    (True, 33, 256, 3, 1e-5, 2, 10), (True, 48, 64, 0, 1e-5, 3, 3), (True, 48, 64, 6, 1e-5, 3, 4),
-    (True, 2, 16, 0, 1e-5, 2, 10), (False, 256, 256, 0, 1e-5, 16, 10), (True, 256, 256, 0, 1e-5, 8, 10)])
-def test_pair_pipeline_equals_stream_pipeline(exact, H, W, stream_wgs, tol, B, n_tv):
-    """The row-pair pipeline (tv_pair_kernel: two rows per pipeline step, single-slot rings between a
-    dual phase and a primal phase) computes exactly what the one-row stream kernel computes (itself
-    bit-identical to the oracle): same samples, block means and TV state, for row splits with halo cuts,
-    odd row counts (a dummy row closes the last pair), narrow images (idle lanes), full-width rows,
-    early stops (tol 3e-2: the last workgroup re-streams stopped planes), 3 <= n_tv < 10 (idle stage waves),
-    H = 2 and full-size batches, in graph replay."""
-    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
-    from psgla_for_posterior_sampling_amd import hip_ops as K
-    g = torch.Generator().manual_seed(8)
-    x = torch.rand((1, 3, H, W), generator=g)
-    dg, y, init, mask2d = orc.inpainting_problem(x, seed_ip=1)
-    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
-    outs = []
-    for variant in ("stream", "pair"):
-        eng = FusedTvChains(init.expand(B, -1, -1, -1).contiguous().to(DEV), y.to(DEV),
-                            mask2d.to(torch.uint8).to(DEV), c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
-                            alpha=1.0, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=n_tv, tol=tol),
-                            seed=3, n_iter=24, n_inter=5, n_inter_mmse=4, exact=exact, kernel_variant=variant,
-                            stream_wgs=stream_wgs)
-        assert eng.main_kernel == ("tv_pair_kernel" if variant == "pair" else "tv_stream_kernel")
-        eng.run(24, graph_steps=8)
-        torch.cuda.synchronize()
-        assert int(eng.sched.d_step.item()) == 24 and int(eng.work.arrive[0].item()) == 0
-        assert float(eng.work.norms.abs().sum()) == 0.0
-        bm, bm2 = eng.blocks()
-        outs.append((eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone()))
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
 
 
 def test_auto_dispatch_by_shape():

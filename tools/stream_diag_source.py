@@ -1,7 +1,9 @@
 """Diagnostic variant of csrc/psgla_kernels.hip (never built into the product library): per-wave cycle
 accounting of the row-stream kernel (tv_stream_kernel): work / wait per step, and the front waves' work
 per pipeline phase.  Exports psgla_diag_set_buffer(device_ptr) for a caller-allocated
-[workgroups][16][8] u64 buffer.  Usage as tools/pair_diag_source.py."""
+[workgroups][16][8] u64 buffer.  Usage:
+    python3 tools/stream_diag_source.py /tmp/diag/psgla_diag.hip   (then hipcc it like build.py does;
+    tools/stream_diag.py loads the result)."""
 import os
 import sys
 
@@ -16,8 +18,8 @@ def rep(old, new, count=1):
     s = s.replace(old, new)
 
 
-rep("""    int pair;                       // stream kernel: 1 = the row-pair pipeline (tv_pair_kernel)
-""", """    int pair;                       // stream kernel: 1 = the row-pair pipeline (tv_pair_kernel)
+rep("""    int fin_inline;                 // stream kernel: 1 = the last workgroup finalises the step
+""", """    int fin_inline;                 // stream kernel: 1 = the last workgroup finalises the step
     unsigned long long* diag;
 """)
 rep("""struct StepInfo {""", """struct Diag { unsigned long long t0 = 0, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; };
