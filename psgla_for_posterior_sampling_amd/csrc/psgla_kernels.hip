@@ -646,7 +646,7 @@ __device__ __forceinline__ void st_nt(float* p, const float4& v) {
 
 // Output store of the tile kernel: write-through (sc1) by default -- all its workgroups finish together
 // and each then releases (writes back) its XCD's dirty L2 lines before the arrival count, which
-// write-through stores leave clean; -DPSGLA_TILE_ST_NT: nt stores as the stream kernel.
+// write-through stores leave clean (nt stores, as the stream kernel's, measured 17 % slower here).
 __device__ __forceinline__ void st_tile(float* p, const float4& v) {
     const v4f x = {v.x, v.y, v.z, v.w};
     asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(x) : "memory");
@@ -1090,7 +1090,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
             const SegGeo g = seg_geo<GEN>(a, rc.p);
             const int gjr = GEN ? min(g.f0 + CPL * lane, L - CPL) : gjc;
             const int bb = g.rp / C;
-            // 64-bit per-lane addresses (default; the SGPR-base form, -DPSGLA_STREAM_SADDR, measured +12 %:
+            // 64-bit per-lane addresses (the SGPR-base form measured +12 % in round 2:
             // this kernel's row cursor sits in VGPRs, so each DMA pays two readfirstlane + 5 wait states)
             const size_t base = plane_off(g.rp) + (size_t)rr * L + gjr;
             if (part == 0) {
@@ -1239,7 +1239,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         const int nst = 3 + (ALPHA1 ? 0 : 1) + ((si.acc && (si.blockend || si.liveout)) ? 2 : 0) + (si.sample ? 1 : 0);
         // a row's stores are spread over the wave's two steps: state + accumulators, then the rest
         bool hold = false, hcore = core;
-        size_t h_base = 0;                  // per-lane element index (PSGLA_STREAM_SADDR: the row's uniform base)
+        size_t h_base = 0;                  // per-lane element index
         uint32_t h_vo = 0;                  // the lane's column as a byte offset
         float4 hM = zero4, hQ = zero4, hX = zero4;
         auto flush_held = [&]() {
