@@ -1454,7 +1454,10 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
 // computed while they fly; mean / sq LDS-DMA'd straight into LDS), 16-byte accumulator updates and
 // the step finalised by the last workgroup (no second launch).  The per-element arithmetic is
 // the stream kernel's in both modes (exact: bit-identical to the oracle; fast: bit-identical to
-// the fast stream kernel).  W <= 256, W % 4 == 0; halos only at cuts inside a plane.
+// the fast stream kernel).  Halos only at cuts inside a plane.  GEN: rows padded to a pitch ldw
+// (W % 4 != 0) and / or column segments (W > 256) -- the stream kernel's segment geometry: tile =
+// (plane, column segment, band), each segment's 256-column window carries n_tv halo columns at
+// interior cuts.
 // ---------------------------------------------------------------------------------------
 template <int R>
 struct TileShared {
@@ -1466,21 +1469,29 @@ struct TileShared {
     int s_flag, s_item, s_next;
 };
 
-template <bool EXACT, bool ALPHA1, int R>
-__device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int plane, int band, int n_it,
+template <bool EXACT, bool ALPHA1, int R, bool GEN>
+__device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int plane, int seg, int band, int n_it,
                                         bool track, long long step, bool fresh) {
     float x2[R][CPL], u0[R][CPL], u1[R][CPL];
     double* const nrm = a.norms;
     const int lane = threadIdx.x & (WAVE - 1);
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int H = a.H, W = a.W, C = a.C, h = a.halo;
+    const int L = GEN ? a.ldw : W;                     // row pitch
     const int b = plane / C, c = plane - b * C;
     const int r0 = band * a.band_h, r1 = min(H, r0 + a.band_h);
     const int e0 = max(0, r0 - h), e1 = min(H, r1 + h);
-    const int gj0 = CPL * lane;
-    const int gjc = min(gj0, W - CPL);                 // DMA source column (every lane in bounds)
+    // column window of the segment: core columns [cc0, cc1), wave window [f0, f0 + 256)
+    const int cc0 = GEN ? seg * a.st_seg_w : 0;
+    const int cc1 = GEN ? min(W, cc0 + a.st_seg_w) : W;
+    const int f0 = GEN ? (max(0, cc0 - a.st_halo) & ~3) : 0;
+    const int gj0 = f0 + CPL * lane;
+    const int gjc = min(gj0, L - CPL);                 // DMA source column (every lane in bounds)
     const bool colok = gj0 < W;
-    const size_t HW = (size_t)H * W;
+    const bool corelane = GEN ? (colok && gj0 >= cc0 && gj0 < cc1) : colok;
+    const int nreal = min(CPL, max(0, W - gj0));      // GEN: the lane's image (non-padding) columns
+    const int lastk = W - 1 - gj0;                    // 0..3 on the lane holding column W-1
+    const size_t HW = (size_t)H * L;
     const size_t E = (size_t)C * HW;
     const size_t BE = (size_t)a.B * E;
     const size_t poff = (size_t)plane * HW;
@@ -1503,22 +1514,22 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
         fX[r] = fY[r] = fU0[r] = fU1[r] = fXS[r] = zero4;
         fM[r] = 0u;
         if (rv[r] && colok) {
-            const size_t base = poff + (size_t)gi[r] * W + gj0;
+            const size_t base = poff + (size_t)gi[r] * L + gj0;
             fX[r] = ld4(a.x[par_in] + base);
             if (!fresh) {
                 fU0[r] = ld4(a.u2[par_in] + 2 * base);
                 fU1[r] = ld4(a.u2[par_in] + 2 * base + 4);
                 if (!ALPHA1) fXS[r] = ld4(a.x2[par_in] + base);
             }
-            fY[r] = ld4(a.yobs + (size_t)b * a.y_cs + (size_t)c * HW + (size_t)gi[r] * W + gj0);
-            fM[r] = *reinterpret_cast<const uint32_t*>(a.mask + (size_t)b * a.m_cs + (size_t)gi[r] * W + gj0);
+            fY[r] = ld4(a.yobs + (size_t)b * a.y_cs + (size_t)c * HW + (size_t)gi[r] * L + gj0);
+            fM[r] = *reinterpret_cast<const uint32_t*>(a.mask + (size_t)b * a.m_cs + (size_t)gi[r] * L + gj0);
         }
     }
     if (need_prev && n_it >= 0) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             if (rv[r] && core[r]) {
-                const size_t base = poff + (size_t)gi[r] * W + gjc;
+                const size_t base = poff + (size_t)gi[r] * L + gjc;
                 glds16(a.mean[par_in] + base, &sh.mst[w * R + r][0][0]);
                 glds16(a.sq[par_in] + base, &sh.mst[w * R + r][1][0]);
             }
@@ -1528,8 +1539,20 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
     float Zn[R][CPL];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
+        // element index in the chain's unpadded C*H*W image: the noise does not depend on the row pitch
         const size_t e = ((size_t)c * H + (rv[r] ? gi[r] : 0)) * W + gj0;
         normal_quad(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)(e >> 2), Zn[r]);
+        if (GEN) {
+            const int esh = (int)(e & 3);               // the same for every lane of the row
+            if (esh != 0) {                             // the lane's 4 elements span two quads
+                float zq[CPL];
+                normal_quad(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)(e >> 2) + 1u, zq);
+                const float w8[8] = {Zn[r][0], Zn[r][1], Zn[r][2], Zn[r][3], zq[0], zq[1], zq[2], zq[3]};
+#pragma unroll
+                for (int i = 0; i < CPL; ++i)
+                    Zn[r][i] = esh == 1 ? w8[i + 1] : (esh == 2 ? w8[i + 2] : w8[i + 3]);
+            }
+        }
     }
     // ---- 3. data term Y = (X + c1 g) + c2 Z, TV start state
 #pragma unroll
@@ -1601,15 +1624,17 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
                 // rel-err terms of the counted rows (row-uniform test; lanes past W are masked once, at
                 // the reduction: adding nothing and adding +0 leave a lane's sum identical)
                 if (trk && core[r] && rv[r]) {
+                    const bool real = !GEN || k < nreal;   // padding columns are not part of the norms
                     if (EXACT) {
-                        const float d = xo - xn;
-                        const float q = xn + 1e-12f;
+                        const float d = real ? xo - xn : 0.f;
+                        const float q = real ? xn + 1e-12f : 0.f;
                         sd = __builtin_fmaf(d, d, sd);
                         sn = __builtin_fmaf(q, q, sn);
                     } else {
-                        const float d = xv - xo;
+                        const float d = real ? xv - xo : 0.f;
+                        const float q = real ? xn : 0.f;
                         sd = __builtin_fmaf(d, d, sd);
-                        sn = __builtin_fmaf(xn, xn, sn);
+                        sn = __builtin_fmaf(q, q, sn);
                     }
                 }
                 z[r][k] = zv;
@@ -1620,7 +1645,7 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
         if (trk) {
             // 16-lane row sums by 4 DPP steps (no readlane round trip before the barrier); the 4 row sums of
             // each wave meet the other waves' at the end of the tile
-            const float2 rs = row_sum2(colok ? sd : 0.f, colok ? sn : 0.f);
+            const float2 rs = row_sum2(corelane ? sd : 0.f, corelane ? sn : 0.f);
             if ((lane & 15) == 0) sh.red[it][w][lane >> 4] = rs;
         }
         __syncthreads();
@@ -1639,7 +1664,8 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
                 const float zr = (k < CPL - 1) ? z[r][k + 1] : zr3;
                 const float g0 = down ? (zd - zc) : 0.0f;
                 float g1 = zr - zc;
-                if (k == CPL - 1) g1 = lastlane ? 0.0f : g1;
+                if (GEN) g1 = (lastk == k) ? 0.0f : g1;     // column W-1: no forward difference
+                else if (k == CPL - 1) g1 = lastlane ? 0.0f : g1;
                 const float uo0 = u0[r][k], uo1 = u1[r][k];
                 if (EXACT) {
                     const float v0 = uo0 + a.sig_tv * g0;
@@ -1677,8 +1703,8 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
     if (need_prev) wait_vm0();                         // this wave's mean / sq DMA landed
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        if (!(rv[r] && core[r] && colok)) continue;
-        const size_t base = poff + (size_t)gi[r] * W + gj0;
+        if (!(rv[r] && core[r] && corelane)) continue;
+        const size_t base = poff + (size_t)gi[r] * L + gj0;
         float Xo[CPL];
 #pragma unroll
         for (int k = 0; k < CPL; ++k)
@@ -1722,19 +1748,26 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
     }
 }
 
-template <bool EXACT, bool ALPHA1, int R>
+template <bool EXACT, bool ALPHA1, int R, bool GEN>
 __global__ void __launch_bounds__(TV_THREADS) tv_tile_kernel(const TvArgs a) {
     __shared__ TileShared<R> sh;
     const long long step = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
     const bool fresh = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
     const int P = a.B * a.C;
-    const int T = a.nbands;
+    const int T = a.nbands * (GEN ? a.st_nsegs : 1);  // tiles per plane: (column segment, band)
     {
-        // all bands of a plane on one XCD (blocks x and x + 8 share one): their halo rows hit its L2
+        // the P * T tiles, plane-major, cut into 8 equal runs, one per XCD (blocks x and x + 8 share one):
+        // the tiles of a plane share an XCD's L2 for their halo rows, and every XCD gets work even when
+        // there are fewer than 8 planes (one image at the CLI's batch 1)
+        const int N = P * T, per = (N + 7) / 8;
         const int x = blockIdx.x, xcd = x & 7, k = x >> 3;
-        const int plane = (k / T) * 8 + xcd;
-        const int band = k - (k / T) * T;
-        if (plane < P) sb_tile<EXACT, ALPHA1, R>(a, sh, plane, band, a.n_tv, true, step, fresh);
+        const int item = xcd * per + k;
+        if (item < N) {
+            const int plane = item / T, t = item - plane * T;
+            const int seg = GEN ? t / a.nbands : 0;
+            const int band = t - seg * a.nbands;
+            sb_tile<EXACT, ALPHA1, R, GEN>(a, sh, plane, seg, band, a.n_tv, true, step, fresh);
+        }
     }
     if (!a.fin_inline) return;
     // ---- step finalisation by the last workgroup to arrive (as tv_stream_kernel) ----
@@ -1781,10 +1814,12 @@ __global__ void __launch_bounds__(TV_THREADS) tv_tile_kernel(const TvArgs a) {
     if (sh.s_item) {
         // rare: redo every tile of a stopped chain with the stopped iteration count (inputs intact)
         for (int item = 0; item < P * T; ++item) {
-            const int plane = item / T, band = item - plane * T;
+            const int plane = item / T, t = item - plane * T;
+            const int seg = GEN ? t / a.nbands : 0;
+            const int band = t - seg * a.nbands;
             const int nstop = __builtin_amdgcn_readfirstlane(sh.s_stop[plane / a.C]);
             if (nstop < a.n_tv) {
-                sb_tile<EXACT, ALPHA1, R>(a, sh, plane, band, nstop, false, step, fresh);
+                sb_tile<EXACT, ALPHA1, R, GEN>(a, sh, plane, seg, band, nstop, false, step, fresh);
                 wait_vm0();
                 __syncthreads();
             }
@@ -2843,10 +2878,11 @@ static int choose_split(long long P, int H, int h, int req, int* out) {
 }
 
 // Small-batch tile kernel geometry: R rows per wave (tile = 16 R rows incl. n_tv halo rows at cuts inside
-// a plane), equal bands per plane.  Returns the number of workgroups (planes rounded up to 8 -- the
-// XCD-aware order -- times bands), 0 if the shape does not fit (W > 256 or W % 4, halo too large).
-static int tile_geometry(int P, int H, int W, int h, int R, int* band_h, int* nbands) {
-    if (W > TV_COLS || (W & 3) || R < 2 || R > 3) return 0;
+// a plane), equal bands per plane, nsegs column segments (stream_segments).  Returns the number of
+// workgroups (tiles rounded up to 8 -- the XCD-aware order), 0 if the shape does not fit (halo too
+// large, no segmentation).
+static int tile_geometry(int P, int H, int nsegs, int h, int R, int* band_h, int* nbands) {
+    if (nsegs < 1 || R != 3) return 0;
     const int rows = TV_NW * R;
     int nb, bh;
     if (H <= rows) {
@@ -2859,7 +2895,7 @@ static int tile_geometry(int P, int H, int W, int h, int R, int* band_h, int* nb
     }
     *band_h = bh;
     *nbands = nb;
-    return ((P + 7) / 8) * 8 * nb;
+    return ((P * nb * nsegs + 7) / 8) * 8;
 }
 
 // Column segments of the streaming kernel: equal core widths (multiples of 4) cut from the image
@@ -2893,11 +2929,11 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
         if (FRONT == FRONT_INPAINT && a.tile_r > 0) {
             TvArgs s = a;
             s.fin_inline = (mask & 2) ? 1 : 0;
-            const int grid = ((P + 7) / 8) * 8 * s.nbands;
-            if (s.tile_r == 2)
-                hipLaunchKernelGGL((tv_tile_kernel<EXACT, ALPHA1, 2>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+            const int grid = ((P * s.nbands * s.st_nsegs + 7) / 8) * 8;   // tile_kernel: 8 runs of tiles
+            if (s.ldw == s.W && s.st_nsegs == 1)
+                hipLaunchKernelGGL((tv_tile_kernel<EXACT, ALPHA1, 3, false>), dim3(grid), dim3(TV_THREADS), 0, st, s);
             else
-                hipLaunchKernelGGL((tv_tile_kernel<EXACT, ALPHA1, 3>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+                hipLaunchKernelGGL((tv_tile_kernel<EXACT, ALPHA1, 3, true>), dim3(grid), dim3(TV_THREADS), 0, st, s);
             return launch_check("tv_tile_kernel");
         }
         if (FRONT == FRONT_INPAINT && a.stream) {
@@ -2938,8 +2974,8 @@ static int check_tv_common(int B, int C, int H, int W, int n_tv) {
 }
 
 // Which fused-step kernel psgla_tv_step launches for a descriptor, and its geometry in `a` (B, C, H, W,
-// ldw and n_tv of `a` set): 0 band kernel (+ finaliser), 1 row stream, 2 row stream with P2P waits,
-// 3 small-batch tile kernel; -1 with g_sel_err on a shape the requested variant does not support.
+// ldw and n_tv of `a` set): 0 band kernel (+ finaliser), 1 row stream, 3 small-batch tile kernel; -1 with
+// g_sel_err on a shape the requested variant does not support.
 static thread_local const char* g_sel_err = "";
 static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
     a.halo = d->n_tv;
@@ -2954,23 +2990,31 @@ static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
     // small-batch tile kernel: forced (variant 4) or, in auto mode, when all tiles fit in one round
     // on the CUs (a row stream would be mostly pipeline fill: strong scaling's 64/N chains per GPU)
     a.tile_r = 0;
+    int tile_segs = 0, tile_sw = 0;
     if (d->kernel_variant == 4 || d->kernel_variant == 0) {
         const int P = d->B * d->C;
         int bh = 0, nb = 0;
-        const int wg = (a.ldw == a.W) ? tile_geometry(P, d->H, d->W, d->n_tv, 3, &bh, &nb) : 0;
+        // column segments as the stream kernel's (one when ldw == W <= 256)
+        tile_segs = (a.ldw % 4 == 0 && d->n_tv >= 1) ? stream_segments(a.W, a.ldw, d->n_tv, &tile_sw) : 0;
+        const int wg = tile_geometry(P, d->H, tile_segs, d->n_tv, 3, &bh, &nb);
         if (d->kernel_variant == 4 && wg == 0) { g_sel_err = "psgla_tv_step: shape not supported by the tile kernel"; return -1; }
-        if (wg > 0 && (d->kernel_variant == 4 || (long long)P * nb <= device_cus())) {
+        if (wg > 0 && (d->kernel_variant == 4 || (long long)P * nb * tile_segs <= device_cus())) {
             a.tile_r = 3;
             a.band_h = bh;
             a.nbands = nb;
             a.nsegs = 1;
-            a.tiles = nb;
+            a.tiles = nb * tile_segs;
             a.stream = 0;
         }
     }
-    if (!a.stream && a.tile_r == 0 && a.ldw != a.W) { g_sel_err = "psgla_tv_step: a row pitch ldw != W needs the streaming kernel"; return -1; }
+    if (!a.stream && a.tile_r == 0 && a.ldw != a.W) { g_sel_err = "psgla_tv_step: a row pitch ldw != W needs the streaming or the tile kernel"; return -1; }
     a.split_wgs = 0;
     a.st_nsegs = 1;
+    if (a.tile_r > 0) {
+        a.st_nsegs = tile_segs;
+        a.st_seg_w = tile_sw;
+        a.st_halo = d->n_tv;
+    }
     if (a.stream) {
         a.st_halo = d->n_tv;
         a.st_nsegs = stream_segments(a.W, a.ldw, d->n_tv, &a.st_seg_w);

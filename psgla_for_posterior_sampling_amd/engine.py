@@ -43,7 +43,7 @@ class FusedTvChains:
         # of the first W columns
         if kernel_variant not in KERNEL_VARIANTS:
             raise ValueError(f"kernel_variant must be one of {sorted(KERNEL_VARIANTS)}")
-        self.ldw = Wd if (Wd % 4 == 0 or kernel_variant in ("band", "tile")) else (Wd + 3) // 4 * 4
+        self.ldw = Wd if (Wd % 4 == 0 or kernel_variant == "band") else (Wd + 3) // 4 * 4
         self.pshape = (B, C, H, self.ldw)
         self.device = dev
         self.alpha = float(alpha)

@@ -736,7 +736,8 @@ def test_stream_segmented_early_stop_exact_vs_oracle():
 
 def test_auto_dispatch_by_shape():
     """64 chains x 3 x 256 x 256 (BASELINE configs[1], one GPU): auto dispatch picks the row stream; 8 chains
-    (the 8-GPU strong split) the tile kernel; alpha != 1 and padded rows the row stream."""
+    (the 8-GPU strong split) the tile kernel; alpha != 1 and many chains of a real shape the row stream; one
+    or two chains of a real shape (padded rows, column segments) the tile kernel."""
     from psgla_for_posterior_sampling_amd.engine import FusedTvChains
     from psgla_for_posterior_sampling_amd import hip_ops as K
 
@@ -749,16 +750,23 @@ def test_auto_dispatch_by_shape():
     assert kern(8, 256, 256) == "tv_tile_kernel"
     assert kern(64, 256, 256, alpha=0.6) == "tv_stream_kernel"
     assert kern(16, 321, 481) == "tv_stream_kernel"
+    assert kern(1, 481, 321) == "tv_tile_kernel"        # castle at the CLI's B = 1: 3 x 2 x 19 tiles
+    assert kern(2, 321, 481) == "tv_tile_kernel"
 
 
 # ------------------------------------------------------------------------------ small-batch tile kernel
 @pytest.mark.parametrize("B,H,W,alpha,tol,n_tv", [(3, 48, 64, 1.0, 1e-5, 10), (2, 100, 64, 1.0, 1e-5, 10),
                                                   (2, 77, 40, 0.6, 1e-5, 10), (2, 40, 52, 1.0, 3e-2, 10),
-                                                  (2, 90, 256, 1.0, 1e-5, 3), (1, 30, 20, 1.0, 1e-5, 14)])
+                                                  (2, 90, 256, 1.0, 1e-5, 3), (1, 30, 20, 1.0, 1e-5, 14),
+                                                  # padded rows / column segments (GEN tiles)
+                                                  (2, 37, 29, 1.0, 1e-5, 10), (1, 60, 300, 1.0, 1e-5, 10),
+                                                  (1, 33, 483, 0.6, 1e-5, 10), (2, 70, 301, 1.0, 3e-2, 10),
+                                                  (1, 50, 257, 1.0, 1e-5, 4), (1, 3, 321, 1.0, 1e-5, 10)])
 def test_tile_kernel_exact_vs_oracle(B, H, W, alpha, tol, n_tv):
     """The small-batch tile kernel (one 48-row tile per workgroup, n_tv halo rows at band cuts, inline
     finalisation) in exact mode: samples, block means and TV state bit-identical to the CPU oracle for
-    band cuts, narrow images (idle lanes), alpha != 1, deepinv's early stop and n_tv > 10."""
+    band cuts, narrow images (idle lanes), alpha != 1, deepinv's early stop and n_tv > 10; and for rows
+    padded to a pitch (W % 4 != 0) and column segments with n_tv halo columns (W > 256)."""
     from psgla_for_posterior_sampling_amd.engine import FusedTvChains
     from psgla_for_posterior_sampling_amd import hip_ops as K
     g = torch.Generator().manual_seed(9)
@@ -807,6 +815,36 @@ def test_tile_kernel_equals_stream_kernel_full_size(B):
                                 alpha=1.0, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10), seed=0,
                                 n_iter=30, n_inter=10, n_inter_mmse=10, exact=exact, kernel_variant=variant)
             eng.run(30, graph_steps=10)
+            torch.cuda.synchronize()
+            bm, bm2 = eng.blocks()
+            outs.append((eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone()))
+        for a, b in zip(*outs):
+            assert torch.equal(a, b), f"exact={exact}"
+
+
+@pytest.mark.parametrize("B,H,W", [(1, 481, 321), (2, 321, 481), (1, 100, 522)])
+def test_tile_kernel_equals_stream_kernel_real_shapes(B, H, W):
+    """The reference's image shapes (set1c castle 481 x 321, CBSD68 321 x 481) at the CLI's batch sizes:
+    the tile kernel with padded rows and column segments gives chains bit-identical to the row-streaming
+    kernel (same segment geometry, same per-element operations), in both arithmetic modes."""
+    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    g = torch.Generator(device=DEV).manual_seed(77)
+    xs = torch.rand((B, 3, H, W), generator=g, device=DEV)
+    gen = torch.Generator(device=DEV).manual_seed(0)
+    mask2d = (torch.rand((H, W), generator=gen, device=DEV) > 0.5).to(torch.uint8)
+    y = mask2d.float() * xs + torch.normal(torch.zeros_like(xs), std=(1 / 255.0) * torch.ones_like(xs),
+                                           generator=gen)
+    init = (mask2d.float() * y + (1 - mask2d.float()) * 0.5).contiguous()
+    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
+    for exact in (True, False):
+        outs = []
+        for variant in ("stream", "tile"):
+            eng = FusedTvChains(init, y.contiguous(), mask2d, c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
+                                alpha=1.0, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10), seed=0,
+                                n_iter=24, n_inter=5, n_inter_mmse=4, exact=exact, kernel_variant=variant)
+            assert eng.main_kernel == "tv_" + variant + "_kernel"
+            eng.run(24, graph_steps=8)
             torch.cuda.synchronize()
             bm, bm2 = eng.blocks()
             outs.append((eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone()))
