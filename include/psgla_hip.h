@@ -72,8 +72,9 @@ typedef struct PsglaSchedule {
  * k >= 2, per chain: the affected chains are recomputed with k+1 inner iterations)
  * is honoured, `fresh` is cleared and *d_step advanced once the step is complete.
  * What is launched depends on the variant the shape selects (kernel_variant 0):
- *   - the small-batch tile kernel (tv_tile_kernel: W <= 256, W % 4 == 0) when its
- *     48-row tiles all fit on the CUs at once (few chains per GPU): ONE launch; its last
+ *   - the small-batch tile kernel (tv_tile_kernel: any W, rows padded to the pitch ldw and cut
+ *     into the stream kernel's column segments when W > 256) when its 48-row tiles all fit on
+ *     the CUs at once (few chains per GPU, or one / two real-size images): ONE launch; its last
  *     workgroup to finish evaluates the early stop, recomputes stopped chains and advances
  *     the step (no second kernel);
  *   - else the row-streaming kernel (tv_stream_kernel: row pitch ldw % 4 == 0,
@@ -112,15 +113,15 @@ typedef struct PsglaTvStep {
                                  idempotent, for kernel timing); 2: finaliser only            */
     int32_t kernel_variant;   /* 0: auto (see above); 1: force the band kernel; 2: force the row stream
                                  (one row per pipeline step); 4: force the small-batch tile kernel
-                                 (W <= 256, W % 4 == 0, ldw == W).  Other values (3 included: the
-                                 row-pair pipeline of ABI 6 is gone) are rejected. */
+                                 (ldw % 4 == 0).  Other values (3 included: the row-pair pipeline
+                                 of ABI 6 is gone) are rejected. */
     int32_t stream_wgs;       /* streaming kernel work split: 0 auto (rows of all planes cut into
                                  one contiguous range per CU, n_tv halo rows at cuts, when W <= 256);
                                  -1 one workgroup per plane; > 0 force that many row ranges      */
     int32_t ldw;              /* row pitch (elements) of every (.., H, W) buffer: x, u2 (x2 per
                                  element pair), x2, mean, sq, y, mask, samples, blocks; 0 = W.
                                  ldw != W (a multiple of 4 >= W: rows padded so that W % 4 != 0
-                                 images run on the streaming kernel) needs the streaming kernel;
+                                 images run on the streaming / tile kernels) needs one of them;
                                  the padding columns are scratch (never read into the image).
                                  The noise stream is indexed by the unpadded element.            */
 } PsglaTvStep;

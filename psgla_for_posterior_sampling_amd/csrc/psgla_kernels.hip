@@ -1599,48 +1599,62 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
         const bool act_d = wr1 > r0 - span && wr0 < r1 + span;
         // primal: x = prox_tau_fx(x2 - tau nabla^T u2, Y); z = 2x - x2; x2 += rho (x - x2)
         const float4 up = (w > 0) ? sh.urow[w - 1][lane] : zero4;
+        // Two instantiations: untracked iterations carry no rel-err arithmetic; tracked ones sum each row
+        // alone and add the counted rows' sums under a row-uniform select (per-element selects otherwise:
+        // the compiler if-converts the row test into the element loop)
+        auto primal_rows = [&](auto trk_tag) __attribute__((always_inline)) {
+            constexpr bool TRK = decltype(trk_tag)::value;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (!act_p) break;
-            const float u1l = __int_as_float(
-                __builtin_amdgcn_update_dpp(0, __float_as_int(u1[r][CPL - 1]), 0x138 /* wave_shr:1 */, 0xF, 0xF, true));
+            for (int r = 0; r < R; ++r) {
+                if (!act_p) break;
+                const float u1l = __int_as_float(
+                    __builtin_amdgcn_update_dpp(0, __float_as_int(u1[r][CPL - 1]), 0x138 /* wave_shr:1 */, 0xF, 0xF, true));
+                float rd = 0.f, rn = 0.f;
 #pragma unroll
-            for (int k = 0; k < CPL; ++k) {
-                // the row above: 0 above the tile's first row (the plane's top row or an artificial halo edge)
-                const float pu = (r > 0) ? u0[r - 1][k] : f4get(up, k);
-                const float u1left = (k > 0) ? u1[r][k - 1] : u1l;
-                const float tt = ((pu - u0[r][k]) - u1[r][k]) + u1left;
-                const float xo = x2[r][k];
-                float xv, zv, xn;
-                if (EXACT) {
-                    xv = ((xo - a.tau * tt) + a.tau * yv[r][k]) / a.opt;
-                    zv = 2.0f * xv - xo;
-                    xn = xo + a.rho * (xv - xo);
-                } else {
-                    xv = __builtin_fmaf(a.tau, yv[r][k] - tt, xo) * a.inv_opt;
-                    zv = __builtin_fmaf(2.0f, xv, -xo);
-                    xn = __builtin_fmaf(a.rho, xv - xo, xo);
-                }
-                // rel-err terms of the counted rows (row-uniform test; lanes past W are masked once, at
-                // the reduction: adding nothing and adding +0 leave a lane's sum identical)
-                if (trk && core[r] && rv[r]) {
-                    const bool real = !GEN || k < nreal;   // padding columns are not part of the norms
+                for (int k = 0; k < CPL; ++k) {
+                    // the row above: 0 above the tile's first row (the plane's top row or an artificial halo edge)
+                    const float pu = (r > 0) ? u0[r - 1][k] : f4get(up, k);
+                    const float u1left = (k > 0) ? u1[r][k - 1] : u1l;
+                    const float tt = ((pu - u0[r][k]) - u1[r][k]) + u1left;
+                    const float xo = x2[r][k];
+                    float xv, zv, xn;
                     if (EXACT) {
-                        const float d = real ? xo - xn : 0.f;
-                        const float q = real ? xn + 1e-12f : 0.f;
-                        sd = __builtin_fmaf(d, d, sd);
-                        sn = __builtin_fmaf(q, q, sn);
+                        xv = ((xo - a.tau * tt) + a.tau * yv[r][k]) / a.opt;
+                        zv = 2.0f * xv - xo;
+                        xn = xo + a.rho * (xv - xo);
                     } else {
-                        const float d = real ? xv - xo : 0.f;
-                        const float q = real ? xn : 0.f;
-                        sd = __builtin_fmaf(d, d, sd);
-                        sn = __builtin_fmaf(q, q, sn);
+                        xv = __builtin_fmaf(a.tau, yv[r][k] - tt, xo) * a.inv_opt;
+                        zv = __builtin_fmaf(2.0f, xv, -xo);
+                        xn = __builtin_fmaf(a.rho, xv - xo, xo);
                     }
+                    if constexpr (TRK) {
+                        const bool real = !GEN || k < nreal;   // padding columns are not part of the norms
+                        if (EXACT) {
+                            const float d = real ? xo - xn : 0.f;
+                            const float q = real ? xn + 1e-12f : 0.f;
+                            rd = __builtin_fmaf(d, d, rd);
+                            rn = __builtin_fmaf(q, q, rn);
+                        } else {
+                            const float d = real ? xv - xo : 0.f;
+                            const float q = real ? xn : 0.f;
+                            rd = __builtin_fmaf(d, d, rd);
+                            rn = __builtin_fmaf(q, q, rn);
+                        }
+                    }
+                    z[r][k] = zv;
+                    x2[r][k] = xn;
                 }
-                z[r][k] = zv;
-                x2[r][k] = xn;
+                // rel-err terms of the counted rows (lanes past W / outside the core are masked once, at the
+                // reduction)
+                if constexpr (TRK) {
+                    const bool rowtrk = core[r] && rv[r];
+                    sd += rowtrk ? rd : 0.f;
+                    sn += rowtrk ? rn : 0.f;
+                }
             }
-        }
+        };
+        if (trk) primal_rows(std::true_type{});
+        else primal_rows(std::false_type{});
         if (act_p) sh.zrow[w][lane] = make_float4(z[0][0], z[0][1], z[0][2], z[0][3]);
         if (trk) {
             // 16-lane row sums by 4 DPP steps (no readlane round trip before the barrier); the 4 row sums of
@@ -2998,7 +3012,12 @@ static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
         tile_segs = (a.ldw % 4 == 0 && d->n_tv >= 1) ? stream_segments(a.W, a.ldw, d->n_tv, &tile_sw) : 0;
         const int wg = tile_geometry(P, d->H, tile_segs, d->n_tv, 3, &bh, &nb);
         if (d->kernel_variant == 4 && wg == 0) { g_sel_err = "psgla_tv_step: shape not supported by the tile kernel"; return -1; }
-        if (wg > 0 && (d->kernel_variant == 4 || (long long)P * nb * tile_segs <= device_cus())) {
+        // auto: the tiles fit in one round on the CUs -- or in two when the rows need column segments (W > 256),
+        // where the row stream's 256-column windows run a third of their lanes idle (measured: castle-size
+        // images at B = 3-4 and 321 x 481 at B = 4-6 run faster as two rounds of tiles; 256 x 256 does not,
+        // profiles/r03l_tile_threshold.txt)
+        const long long ntiles = (long long)P * nb * tile_segs, cus = device_cus();
+        if (wg > 0 && (d->kernel_variant == 4 || ntiles <= cus || (tile_segs > 1 && ntiles <= 2 * cus))) {
             a.tile_r = 3;
             a.band_h = bh;
             a.nbands = nb;

@@ -752,6 +752,9 @@ def test_auto_dispatch_by_shape():
     assert kern(16, 321, 481) == "tv_stream_kernel"
     assert kern(1, 481, 321) == "tv_tile_kernel"        # castle at the CLI's B = 1: 3 x 2 x 19 tiles
     assert kern(2, 321, 481) == "tv_tile_kernel"
+    assert kern(4, 481, 321) == "tv_tile_kernel"        # two rounds of tiles beat segmented row streams
+    assert kern(8, 481, 321) == "tv_stream_kernel"
+    assert kern(12, 256, 256) == "tv_stream_kernel"     # unsegmented rows: one round of tiles at most
 
 
 # ------------------------------------------------------------------------------ small-batch tile kernel
