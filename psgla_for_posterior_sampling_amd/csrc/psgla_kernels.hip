@@ -1599,62 +1599,48 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
         const bool act_d = wr1 > r0 - span && wr0 < r1 + span;
         // primal: x = prox_tau_fx(x2 - tau nabla^T u2, Y); z = 2x - x2; x2 += rho (x - x2)
         const float4 up = (w > 0) ? sh.urow[w - 1][lane] : zero4;
-        // Two instantiations: untracked iterations carry no rel-err arithmetic; tracked ones sum each row
-        // alone and add the counted rows' sums under a row-uniform select (per-element selects otherwise:
-        // the compiler if-converts the row test into the element loop)
-        auto primal_rows = [&](auto trk_tag) __attribute__((always_inline)) {
-            constexpr bool TRK = decltype(trk_tag)::value;
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                if (!act_p) break;
-                const float u1l = __int_as_float(
-                    __builtin_amdgcn_update_dpp(0, __float_as_int(u1[r][CPL - 1]), 0x138 /* wave_shr:1 */, 0xF, 0xF, true));
-                float rd = 0.f, rn = 0.f;
+        for (int r = 0; r < R; ++r) {
+            if (!act_p) break;
+            const float u1l = __int_as_float(
+                __builtin_amdgcn_update_dpp(0, __float_as_int(u1[r][CPL - 1]), 0x138 /* wave_shr:1 */, 0xF, 0xF, true));
 #pragma unroll
-                for (int k = 0; k < CPL; ++k) {
-                    // the row above: 0 above the tile's first row (the plane's top row or an artificial halo edge)
-                    const float pu = (r > 0) ? u0[r - 1][k] : f4get(up, k);
-                    const float u1left = (k > 0) ? u1[r][k - 1] : u1l;
-                    const float tt = ((pu - u0[r][k]) - u1[r][k]) + u1left;
-                    const float xo = x2[r][k];
-                    float xv, zv, xn;
+            for (int k = 0; k < CPL; ++k) {
+                // the row above: 0 above the tile's first row (the plane's top row or an artificial halo edge)
+                const float pu = (r > 0) ? u0[r - 1][k] : f4get(up, k);
+                const float u1left = (k > 0) ? u1[r][k - 1] : u1l;
+                const float tt = ((pu - u0[r][k]) - u1[r][k]) + u1left;
+                const float xo = x2[r][k];
+                float xv, zv, xn;
+                if (EXACT) {
+                    xv = ((xo - a.tau * tt) + a.tau * yv[r][k]) / a.opt;
+                    zv = 2.0f * xv - xo;
+                    xn = xo + a.rho * (xv - xo);
+                } else {
+                    xv = __builtin_fmaf(a.tau, yv[r][k] - tt, xo) * a.inv_opt;
+                    zv = __builtin_fmaf(2.0f, xv, -xo);
+                    xn = __builtin_fmaf(a.rho, xv - xo, xo);
+                }
+                // rel-err terms of the counted rows (row-uniform test; lanes past W are masked once, at
+                // the reduction: adding nothing and adding +0 leave a lane's sum identical)
+                if (trk && core[r] && rv[r]) {
+                    const bool real = !GEN || k < nreal;   // padding columns are not part of the norms
                     if (EXACT) {
-                        xv = ((xo - a.tau * tt) + a.tau * yv[r][k]) / a.opt;
-                        zv = 2.0f * xv - xo;
-                        xn = xo + a.rho * (xv - xo);
+                        const float d = real ? xo - xn : 0.f;
+                        const float q = real ? xn + 1e-12f : 0.f;
+                        sd = __builtin_fmaf(d, d, sd);
+                        sn = __builtin_fmaf(q, q, sn);
                     } else {
-                        xv = __builtin_fmaf(a.tau, yv[r][k] - tt, xo) * a.inv_opt;
-                        zv = __builtin_fmaf(2.0f, xv, -xo);
-                        xn = __builtin_fmaf(a.rho, xv - xo, xo);
+                        const float d = real ? xv - xo : 0.f;
+                        const float q = real ? xn : 0.f;
+                        sd = __builtin_fmaf(d, d, sd);
+                        sn = __builtin_fmaf(q, q, sn);
                     }
-                    if constexpr (TRK) {
-                        const bool real = !GEN || k < nreal;   // padding columns are not part of the norms
-                        if (EXACT) {
-                            const float d = real ? xo - xn : 0.f;
-                            const float q = real ? xn + 1e-12f : 0.f;
-                            rd = __builtin_fmaf(d, d, rd);
-                            rn = __builtin_fmaf(q, q, rn);
-                        } else {
-                            const float d = real ? xv - xo : 0.f;
-                            const float q = real ? xn : 0.f;
-                            rd = __builtin_fmaf(d, d, rd);
-                            rn = __builtin_fmaf(q, q, rn);
-                        }
-                    }
-                    z[r][k] = zv;
-                    x2[r][k] = xn;
                 }
-                // rel-err terms of the counted rows (lanes past W / outside the core are masked once, at the
-                // reduction)
-                if constexpr (TRK) {
-                    const bool rowtrk = core[r] && rv[r];
-                    sd += rowtrk ? rd : 0.f;
-                    sn += rowtrk ? rn : 0.f;
-                }
+                z[r][k] = zv;
+                x2[r][k] = xn;
             }
-        };
-        if (trk) primal_rows(std::true_type{});
-        else primal_rows(std::false_type{});
+        }
         if (act_p) sh.zrow[w][lane] = make_float4(z[0][0], z[0][1], z[0][2], z[0][3]);
         if (trk) {
             // 16-lane row sums by 4 DPP steps (no readlane round trip before the barrier); the 4 row sums of
