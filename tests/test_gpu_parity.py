@@ -734,6 +734,44 @@ def test_stream_segmented_early_stop_exact_vs_oracle():
     assert fired, "test needs the early stop to fire"
 
 
+@pytest.mark.parametrize("variant", ["stream", "tile", "band"])
+def test_fused_single_channel_exact_vs_oracle(variant):
+    """One-channel (grayscale, --grayscale) images: the fused step with C = 1 is bit-identical to the oracle
+    on the same data term (-mask * (x - y) / sigma2, sampling_images.py:295 with a one-channel mask)."""
+    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    H, W, B, n_iter = 40, 52, 2, 12
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand((1, 1, H, W), generator=g)
+    gm = torch.Generator().manual_seed(3)
+    mask_2d = 1 * (torch.rand((H, W), generator=gm) > 0.5)
+    mask = torch.ones(1)[None, :, None, None] * mask_2d[None, None, :, :]
+    sigma1 = 1 / 255.0
+    sigma2t = torch.tensor(sigma1 ** 2, dtype=torch.float32)
+    y = mask * x + torch.normal(torch.zeros(*x.size()), std=sigma1 * torch.ones(*x.size()), generator=gm)
+    init = mask * y + (1 - mask) * 0.5 * torch.ones(y.shape)
+
+    def dg(v):
+        return -mask * (v - y) / sigma2t
+    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
+    eng = FusedTvChains(init.expand(B, -1, -1, -1).contiguous().to(DEV), y.to(DEV), mask_2d.to(torch.uint8).to(DEV),
+                        c1=c1, c2=c2, sigma2=float(np.float32(sigma1 ** 2)), alpha=1.0, ths=float(np.float32(10 / 255.0)),
+                        tv=K.TvConstants(n_it_max=10), seed=7, n_iter=n_iter, n_inter=3, n_inter_mmse=2, exact=True,
+                        kernel_variant=variant)
+    assert eng.main_kernel == {"stream": "tv_stream_kernel", "tile": "tv_tile_kernel", "band": "tv_main_kernel"}[variant]
+    eng.run(n_iter, graph_steps=0)
+    torch.cuda.synchronize()
+    bm, bm2 = eng.blocks()
+    for b in range(B):
+        tv = orc.TVDenoiser(n_it_max=10)
+        Xl, Ml, M2l = orc.psgla(init, dg, tv, torch.tensor(1.0), torch.tensor(10.0), sig_float=10 / 255.0,
+                                delta=(10 / 255.0) ** 2, n_iter=n_iter, n_inter=3, n_inter_mmse=2, seed=7, chain=b)
+        # the oracle's lists hold squeezed tensors (restoration_algorithms.py:244: torch.squeeze drops C = 1)
+        np.testing.assert_array_equal(eng.samples()[:, b, 0].cpu().numpy(), np.stack([t.numpy() for t in Xl]))
+        np.testing.assert_array_equal(bm[:, b, 0].cpu().numpy(), np.stack([t.numpy() for t in Ml]))
+        np.testing.assert_array_equal(bm2[:, b, 0].cpu().numpy(), np.stack([t.numpy() for t in M2l]))
+
+
 def test_auto_dispatch_by_shape():
     """64 chains x 3 x 256 x 256 (BASELINE configs[1], one GPU): auto dispatch picks the row stream; 8 chains
     (the 8-GPU strong split) the tile kernel; alpha != 1 and many chains of a real shape the row stream; one
