@@ -63,3 +63,38 @@ def test_no_cpu_fallback_without_library(monkeypatch):
     monkeypatch.setattr(N, "LIB_PATH", "/nonexistent/libpsgla_hip.so")
     with pytest.raises(N.NativeLibraryError):
         N.lib()
+
+
+def test_kernel_dispatch_rules_on_the_host():
+    """psgla_tv_step_kernel is a host-side query (launches nothing; without a GPU the CU count defaults to the
+    MI355X's 256): the fused-step kernel choice for the bench shape, the strong-scaling split, the reference's
+    image shapes at the CLI's batch sizes, forced variants and the rejected ones."""
+    from psgla_for_posterior_sampling_amd import _native as N
+    lib = N.lib()
+    BAND, STREAM, TILE = 0, 1, 3
+
+    def kind(B, H, W, ldw=0, n_tv=10, variant=0, alpha1=True):
+        d = N.PsglaTvStep()
+        d.B, d.C, d.H, d.W, d.ldw, d.n_tv, d.kernel_variant = B, 3, H, W, ldw, n_tv, variant
+        if not alpha1:
+            d.x2[0], d.x2[1] = 16, 32          # non-null: alpha != 1 (the query never dereferences them)
+        k = lib.psgla_tv_step_kernel(ctypes.byref(d))
+        return k, (lib.psgla_last_error().decode() if k < 0 else "")
+
+    assert kind(64, 256, 256)[0] == STREAM                       # BASELINE configs[1], one GPU
+    assert kind(8, 256, 256)[0] == TILE                          # 8-GPU strong split: 240 tiles
+    assert kind(12, 256, 256)[0] == STREAM                       # 360 tiles: two rounds lose to the stream
+    assert kind(64, 256, 256, alpha1=False)[0] == STREAM
+    assert kind(1, 481, 321, ldw=324)[0] == TILE                 # castle at the CLI's batch 1
+    assert kind(4, 481, 321, ldw=324)[0] == TILE                 # segmented rows: two rounds of tiles
+    assert kind(8, 481, 321, ldw=324)[0] == STREAM
+    assert kind(2, 321, 481, ldw=484)[0] == TILE
+    assert kind(1, 256, 256, n_tv=14)[0] == TILE                 # n_tv > 10: no stream kernel
+    assert kind(64, 256, 256, n_tv=14)[0] == BAND
+    assert kind(64, 256, 256, variant=4)[0] == TILE              # forced variants
+    assert kind(64, 256, 256, variant=1)[0] == BAND
+    assert kind(8, 256, 256, variant=2)[0] == STREAM
+    k, err = kind(64, 256, 256, variant=3)                       # the row-pair pipeline is gone (ABI 7)
+    assert k == -1 and "kernel_variant" in err
+    k, err = kind(1, 481, 321, ldw=324, variant=1)               # the band kernel needs ldw == W
+    assert k == -1 and "row pitch" in err
