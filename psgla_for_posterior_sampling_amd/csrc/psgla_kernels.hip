@@ -2885,7 +2885,7 @@ static int choose_split(long long P, int H, int h, int req, int* out) {
 // workgroups (tiles rounded up to 8 -- the XCD-aware order), 0 if the shape does not fit (halo too
 // large, no segmentation).
 static int tile_geometry(int P, int H, int nsegs, int h, int R, int* band_h, int* nbands) {
-    if (nsegs < 1 || R != 3) return 0;
+    if (nsegs < 1 || R < 2 || R > 3) return 0;
     const int rows = TV_NW * R;
     int nb, bh;
     if (H <= rows) {
@@ -2933,10 +2933,14 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
             TvArgs s = a;
             s.fin_inline = (mask & 2) ? 1 : 0;
             const int grid = ((P * s.nbands * s.st_nsegs + 7) / 8) * 8;   // tile_kernel: 8 runs of tiles
-            if (s.ldw == s.W && s.st_nsegs == 1)
-                hipLaunchKernelGGL((tv_tile_kernel<EXACT, ALPHA1, 3, false>), dim3(grid), dim3(TV_THREADS), 0, st, s);
-            else
-                hipLaunchKernelGGL((tv_tile_kernel<EXACT, ALPHA1, 3, true>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+            const bool gen = !(s.ldw == s.W && s.st_nsegs == 1);
+            if (s.tile_r == 2) {
+                if (!gen) hipLaunchKernelGGL((tv_tile_kernel<EXACT, ALPHA1, 2, false>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+                else hipLaunchKernelGGL((tv_tile_kernel<EXACT, ALPHA1, 2, true>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+            } else {
+                if (!gen) hipLaunchKernelGGL((tv_tile_kernel<EXACT, ALPHA1, 3, false>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+                else hipLaunchKernelGGL((tv_tile_kernel<EXACT, ALPHA1, 3, true>), dim3(grid), dim3(TV_THREADS), 0, st, s);
+            }
             return launch_check("tv_tile_kernel");
         }
         if (FRONT == FRONT_INPAINT && a.stream) {
@@ -2999,7 +3003,9 @@ static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
         int bh = 0, nb = 0;
         // column segments as the stream kernel's (one when ldw == W <= 256)
         tile_segs = (a.ldw % 4 == 0 && d->n_tv >= 1) ? stream_segments(a.W, a.ldw, d->n_tv, &tile_sw) : 0;
+        int bh2 = 0, nb2 = 0;
         const int wg = tile_geometry(P, d->H, tile_segs, d->n_tv, 3, &bh, &nb);
+        const int wg2 = tile_geometry(P, d->H, tile_segs, d->n_tv, 2, &bh2, &nb2);
         if (d->kernel_variant == 4 && wg == 0) { g_sel_err = "psgla_tv_step: shape not supported by the tile kernel"; return -1; }
         // auto: the tiles fit in one round on the CUs -- or in two when the rows need column segments (W > 256),
         // where the row stream's 256-column windows run a third of their lanes idle (measured: castle-size
@@ -3010,8 +3016,16 @@ static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
             a.tile_r = 3;
             a.band_h = bh;
             a.nbands = nb;
+            // 32-row tiles (2 rows per wave) when they still fit in one round: one or a few images leave most
+            // CUs idle at 48 rows (castle B = 1: 114 tiles of 48 rows vs 246 of 32 rows, 41.1 -> 35.0 us,
+            // profiles/r03q_tile_r2_ab.txt); more tiles but shorter waves
+            if (wg2 > 0 && (long long)P * nb2 * tile_segs <= cus) {
+                a.tile_r = 2;
+                a.band_h = bh2;
+                a.nbands = nb2;
+            }
             a.nsegs = 1;
-            a.tiles = nb * tile_segs;
+            a.tiles = a.nbands * tile_segs;
             a.stream = 0;
         }
     }

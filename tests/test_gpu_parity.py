@@ -802,12 +802,16 @@ def test_auto_dispatch_by_shape():
                                                   # padded rows / column segments (GEN tiles)
                                                   (2, 37, 29, 1.0, 1e-5, 10), (1, 60, 300, 1.0, 1e-5, 10),
                                                   (1, 33, 483, 0.6, 1e-5, 10), (2, 70, 301, 1.0, 3e-2, 10),
-                                                  (1, 50, 257, 1.0, 1e-5, 4), (1, 3, 321, 1.0, 1e-5, 10)])
+                                                  (1, 50, 257, 1.0, 1e-5, 4), (1, 3, 321, 1.0, 1e-5, 10),
+                                                  # enough tiles that 32-row tiles would need two rounds:
+                                                  # 48-row tiles (3 rows per wave), plain and segmented
+                                                  (24, 100, 64, 1.0, 1e-5, 10), (24, 40, 301, 1.0, 3e-2, 10)])
 def test_tile_kernel_exact_vs_oracle(B, H, W, alpha, tol, n_tv):
-    """The small-batch tile kernel (one 48-row tile per workgroup, n_tv halo rows at band cuts, inline
-    finalisation) in exact mode: samples, block means and TV state bit-identical to the CPU oracle for
-    band cuts, narrow images (idle lanes), alpha != 1, deepinv's early stop and n_tv > 10; and for rows
-    padded to a pitch (W % 4 != 0) and column segments with n_tv halo columns (W > 256)."""
+    """The small-batch tile kernel (one 32- or 48-row tile per workgroup, n_tv halo rows at band cuts,
+    inline finalisation) in exact mode: samples, block means and TV state bit-identical to the CPU oracle
+    for band cuts, narrow images (idle lanes), alpha != 1, deepinv's early stop and n_tv > 10; for rows
+    padded to a pitch (W % 4 != 0) and column segments with n_tv halo columns (W > 256); 32-row tiles
+    where they fit on the CUs in one round, 48-row tiles for the larger batches."""
     from psgla_for_posterior_sampling_amd.engine import FusedTvChains
     from psgla_for_posterior_sampling_amd import hip_ops as K
     g = torch.Generator().manual_seed(9)
