@@ -805,7 +805,10 @@ def test_auto_dispatch_by_shape():
                                                   (1, 50, 257, 1.0, 1e-5, 4), (1, 3, 321, 1.0, 1e-5, 10),
                                                   # enough tiles that 32-row tiles would need two rounds:
                                                   # 48-row tiles (3 rows per wave), plain and segmented
-                                                  (24, 100, 64, 1.0, 1e-5, 10), (24, 40, 301, 1.0, 3e-2, 10)])
+                                                  (24, 100, 64, 1.0, 1e-5, 10), (24, 40, 301, 1.0, 3e-2, 10),
+                                                  # one- and two-row images, one inner iteration
+                                                  (2, 1, 40, 1.0, 1e-5, 10), (1, 2, 321, 1.0, 1e-5, 10),
+                                                  (2, 37, 64, 1.0, 1e-5, 1)])
 def test_tile_kernel_exact_vs_oracle(B, H, W, alpha, tol, n_tv):
     """The small-batch tile kernel (one 32- or 48-row tile per workgroup, n_tv halo rows at band cuts,
     inline finalisation) in exact mode: samples, block means and TV state bit-identical to the CPU oracle
@@ -831,9 +834,11 @@ def test_tile_kernel_exact_vs_oracle(B, H, W, alpha, tol, n_tv):
         tv = orc.TVDenoiser(n_it_max=n_tv, tol=tol)
         Xl, Ml, M2l = orc.psgla(init, dg, tv, torch.tensor(alpha), torch.tensor(10.0), sig_float=10 / 255.0,
                                 delta=(10 / 255.0) ** 2, n_iter=n_iter, n_inter=3, n_inter_mmse=2, seed=6, chain=4 + b)
-        np.testing.assert_array_equal(eng.samples()[:, b].cpu().numpy(), np.stack([t.numpy() for t in Xl]))
-        np.testing.assert_array_equal(bm[:, b].cpu().numpy(), np.stack([t.numpy() for t in Ml]))
-        np.testing.assert_array_equal(bm2[:, b].cpu().numpy(), np.stack([t.numpy() for t in M2l]))
+        # (the oracle's lists hold squeezed tensors: a one-row image loses its H axis there)
+        sm = eng.samples()[:, b].cpu().numpy()
+        np.testing.assert_array_equal(sm, np.stack([t.numpy() for t in Xl]).reshape(sm.shape))
+        np.testing.assert_array_equal(bm[:, b].cpu().numpy(), np.stack([t.numpy() for t in Ml]).reshape(bm[:, b].shape))
+        np.testing.assert_array_equal(bm2[:, b].cpu().numpy(), np.stack([t.numpy() for t in M2l]).reshape(bm2[:, b].shape))
         np.testing.assert_array_equal(eng.x2_state[b].cpu().numpy(), tv.x2.numpy()[0])
         np.testing.assert_array_equal(eng.u2_state[b].cpu().numpy(), tv.u2.numpy()[0])
 
