@@ -97,6 +97,7 @@ struct TvArgs {
     int st_nsegs, st_seg_w, st_halo;  // stream kernel column segmentation (W > 256)
     int fin_inline;                 // stream kernel: 1 = the last workgroup finalises the step
     int tile_r;                     // > 0: small-batch tile kernel with tile_r rows per wave (one tile per workgroup)
+    int tile_nw;                    // tile kernel: waves per workgroup (16 or 8)
 };
 
 // Inner iterations (chunk-local) whose rel_err deepinv tests: global index >= 2 ("it > 1"); in the call's
@@ -1459,18 +1460,22 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
 // (plane, column segment, band), each segment's 256-column window carries n_tv halo columns at
 // interior cuts.
 // ---------------------------------------------------------------------------------------
-template <int R>
+// Core rows whose mean / sq rows a tile stages in LDS: all rows of the tile, at most 56 (112 KB; a 72-row tile
+// of 8 waves x 9 rows has 52 core rows at n_tv = 10 -- tile_geometry keeps band_h within this)
+constexpr int tile_mst_rows(int nw, int r) { return nw * r < 56 ? nw * r : 56; }
+
+template <int R, int NW>
 struct TileShared {
-    float4 zrow[TV_NW][WAVE];          // first-row z of each wave (read by the wave above)
-    float4 urow[TV_NW][WAVE];          // last-row u2[..., 0] of each wave (read by the wave below)
-    float4 mst[TV_NW * R][2][WAVE];    // mean / sq rows of the tile (LDS-DMA at the start)
-    float2 red[MAXIT][TV_NW][4];       // rel_err partial sums per (iteration, wave, 16-lane row of the wave)
+    float4 zrow[NW][WAVE];             // first-row z of each wave (read by the wave above)
+    float4 urow[NW][WAVE];             // last-row u2[..., 0] of each wave (read by the wave below)
+    float4 mst[tile_mst_rows(NW, R)][2][WAVE];   // mean / sq of the tile's core rows (LDS-DMA at the start)
+    float2 red[MAXIT][NW][4];          // rel_err partial sums per (iteration, wave, 16-lane row of the wave)
     int s_stop[MAXG];
     int s_flag, s_item, s_next;
 };
 
-template <bool EXACT, bool ALPHA1, int R, bool GEN>
-__device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int plane, int seg, int band, int n_it,
+template <bool EXACT, bool ALPHA1, int R, bool GEN, int NW>
+__device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, int plane, int seg, int band, int n_it,
                                         bool track, long long step, bool fresh) {
     float x2[R][CPL], u0[R][CPL], u1[R][CPL];
     double* const nrm = a.norms;
@@ -1530,8 +1535,8 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
         for (int r = 0; r < R; ++r) {
             if (rv[r] && core[r]) {
                 const size_t base = poff + (size_t)gi[r] * L + gjc;
-                glds16(a.mean[par_in] + base, &sh.mst[w * R + r][0][0]);
-                glds16(a.sq[par_in] + base, &sh.mst[w * R + r][1][0]);
+                glds16(a.mean[par_in] + base, &sh.mst[gi[r] - r0][0][0]);
+                glds16(a.sq[par_in] + base, &sh.mst[gi[r] - r0][1][0]);
             }
         }
     }
@@ -1653,7 +1658,7 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
         }
         __syncthreads();
         // dual: u = prox_sigma_g_conj(u2 + sigma nabla z, ths); u2 += rho (u - u2)
-        const float4 dn = (w < TV_NW - 1) ? sh.zrow[w + 1][lane] : zero4;
+        const float4 dn = (w < NW - 1) ? sh.zrow[w + 1][lane] : zero4;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             if (!act_d) break;
@@ -1695,7 +1700,7 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
         const int t = threadIdx.x;
         if (t >= trk_lo(a) && t <= trk_hi(a) && t < n_it) {
             double sd = 0.0, sn = 0.0;
-            for (int ww = 0; ww < TV_NW; ++ww)
+            for (int ww = 0; ww < NW; ++ww)
                 for (int q = 0; q < 4; ++q) { sd += sh.red[t][ww][q].x; sn += sh.red[t][ww][q].y; }
             if (!EXACT) sd *= (double)(a.rho * a.rho);     // fast sums hold (x - x2_prev)^2
             atomicAdd(&nrm[((size_t)b * a.n_tv + t) * 2], sd);
@@ -1721,8 +1726,8 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
         if (si.acc) {
             float4 bm = zero4, bq = zero4;
             if (need_prev) {
-                bm = sh.mst[w * R + r][0][lane];
-                bq = sh.mst[w * R + r][1][lane];
+                bm = sh.mst[gi[r] - r0][0][lane];
+                bq = sh.mst[gi[r] - r0][1][lane];
             }
             const float ms[CPL] = {bm.x, bm.y, bm.z, bm.w};
             const float qs[CPL] = {bq.x, bq.y, bq.z, bq.w};
@@ -1751,9 +1756,9 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R>& sh, int 
     }
 }
 
-template <bool EXACT, bool ALPHA1, int R, bool GEN>
-__global__ void __launch_bounds__(TV_THREADS) tv_tile_kernel(const TvArgs a) {
-    __shared__ TileShared<R> sh;
+template <bool EXACT, bool ALPHA1, int R, bool GEN, int NW>
+__global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
+    __shared__ TileShared<R, NW> sh;
     const long long step = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
     const bool fresh = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
     const int P = a.B * a.C;
@@ -1769,7 +1774,7 @@ __global__ void __launch_bounds__(TV_THREADS) tv_tile_kernel(const TvArgs a) {
             const int plane = item / T, t = item - plane * T;
             const int seg = GEN ? t / a.nbands : 0;
             const int band = t - seg * a.nbands;
-            sb_tile<EXACT, ALPHA1, R, GEN>(a, sh, plane, seg, band, a.n_tv, true, step, fresh);
+            sb_tile<EXACT, ALPHA1, R, GEN, NW>(a, sh, plane, seg, band, a.n_tv, true, step, fresh);
         }
     }
     if (!a.fin_inline) return;
@@ -1822,7 +1827,7 @@ __global__ void __launch_bounds__(TV_THREADS) tv_tile_kernel(const TvArgs a) {
             const int band = t - seg * a.nbands;
             const int nstop = __builtin_amdgcn_readfirstlane(sh.s_stop[plane / a.C]);
             if (nstop < a.n_tv) {
-                sb_tile<EXACT, ALPHA1, R, GEN>(a, sh, plane, seg, band, nstop, false, step, fresh);
+                sb_tile<EXACT, ALPHA1, R, GEN, NW>(a, sh, plane, seg, band, nstop, false, step, fresh);
                 wait_vm0();
                 __syncthreads();
             }
@@ -2880,18 +2885,18 @@ static int choose_split(long long P, int H, int h, int req, int* out) {
     return 0;
 }
 
-// Small-batch tile kernel geometry: R rows per wave (tile = 16 R rows incl. n_tv halo rows at cuts inside
-// a plane), equal bands per plane, nsegs column segments (stream_segments).  Returns the number of
-// workgroups (tiles rounded up to 8 -- the XCD-aware order), 0 if the shape does not fit (halo too
-// large, no segmentation).
-static int tile_geometry(int P, int H, int nsegs, int h, int R, int* band_h, int* nbands) {
-    if (nsegs < 1 || R < 2 || R > 3) return 0;
-    const int rows = TV_NW * R;
+// Small-batch tile kernel geometry: NW waves of R rows (tile = NW R rows incl. n_tv halo rows at cuts
+// inside a plane), equal bands per plane, nsegs column segments (stream_segments); a band's core rows
+// stay within the LDS staging of mean / sq (tile_mst_rows).  Returns the number of workgroups (tiles
+// rounded up to 8 -- the XCD-aware order), 0 if the shape does not fit (halo too large, no segmentation).
+static int tile_geometry(int P, int H, int nsegs, int h, int NW, int R, int* band_h, int* nbands) {
+    if (nsegs < 1 || R < 2) return 0;
+    const int rows = NW * R, mst = tile_mst_rows(NW, R);
     int nb, bh;
-    if (H <= rows) {
+    if (H <= mst) {
         nb = 1; bh = H;
     } else {
-        const int core = rows - 2 * h;
+        const int core = min(rows - 2 * h, mst);
         if (core < 1) return 0;
         nb = (H + core - 1) / core;
         bh = (H + nb - 1) / nb;
@@ -2934,14 +2939,19 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
             s.fin_inline = (mask & 2) ? 1 : 0;
             const int grid = ((P * s.nbands * s.st_nsegs + 7) / 8) * 8;   // tile_kernel: 8 runs of tiles
             const bool gen = !(s.ldw == s.W && s.st_nsegs == 1);
-            if (s.tile_r == 2) {
-                if (!gen) hipLaunchKernelGGL((tv_tile_kernel<EXACT, ALPHA1, 2, false>), dim3(grid), dim3(TV_THREADS), 0, st, s);
-                else hipLaunchKernelGGL((tv_tile_kernel<EXACT, ALPHA1, 2, true>), dim3(grid), dim3(TV_THREADS), 0, st, s);
-            } else {
-                if (!gen) hipLaunchKernelGGL((tv_tile_kernel<EXACT, ALPHA1, 3, false>), dim3(grid), dim3(TV_THREADS), 0, st, s);
-                else hipLaunchKernelGGL((tv_tile_kernel<EXACT, ALPHA1, 3, true>), dim3(grid), dim3(TV_THREADS), 0, st, s);
-            }
-            return launch_check("tv_tile_kernel");
+#define PSGLA_TILE(NWV, RV)                                                                                        \
+    if (s.tile_nw == NWV && s.tile_r == RV) {                                                                      \
+        if (!gen) hipLaunchKernelGGL((tv_tile_kernel<EXACT, ALPHA1, RV, false, NWV>), dim3(grid), dim3(NWV * WAVE), 0, st, s); \
+        else hipLaunchKernelGGL((tv_tile_kernel<EXACT, ALPHA1, RV, true, NWV>), dim3(grid), dim3(NWV * WAVE), 0, st, s);       \
+        return launch_check("tv_tile_kernel");                                                                     \
+    }
+            PSGLA_TILE(16, 2)
+            PSGLA_TILE(16, 3)
+            PSGLA_TILE(8, 4)
+            PSGLA_TILE(8, 6)
+            PSGLA_TILE(8, 9)
+#undef PSGLA_TILE
+            return fail(0, "psgla_tv_step: internal error: no tile kernel of this shape");
         }
         if (FRONT == FRONT_INPAINT && a.stream) {
             TvArgs s = a;
@@ -2997,30 +3007,43 @@ static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
     // small-batch tile kernel: forced (variant 4) or, in auto mode, when all tiles fit in one round
     // on the CUs (a row stream would be mostly pipeline fill: strong scaling's 64/N chains per GPU)
     a.tile_r = 0;
+    a.tile_nw = 16;
     int tile_segs = 0, tile_sw = 0;
     if (d->kernel_variant == 4 || d->kernel_variant == 0) {
         const int P = d->B * d->C;
         int bh = 0, nb = 0;
         // column segments as the stream kernel's (one when ldw == W <= 256)
         tile_segs = (a.ldw % 4 == 0 && d->n_tv >= 1) ? stream_segments(a.W, a.ldw, d->n_tv, &tile_sw) : 0;
-        int bh2 = 0, nb2 = 0;
-        const int wg = tile_geometry(P, d->H, tile_segs, d->n_tv, 3, &bh, &nb);
-        const int wg2 = tile_geometry(P, d->H, tile_segs, d->n_tv, 2, &bh2, &nb2);
+        int bh2 = 0, nb2 = 0, bh9 = 0, nb9 = 0;
+        const int wg = tile_geometry(P, d->H, tile_segs, d->n_tv, 16, 3, &bh, &nb);
+        const int wg2 = tile_geometry(P, d->H, tile_segs, d->n_tv, 16, 2, &bh2, &nb2);
+        const int wg9 = tile_geometry(P, d->H, tile_segs, d->n_tv, 8, 9, &bh9, &nb9);
         if (d->kernel_variant == 4 && wg == 0) { g_sel_err = "psgla_tv_step: shape not supported by the tile kernel"; return -1; }
         // auto: the tiles fit in one round on the CUs -- or in two when the rows need column segments (W > 256),
         // where the row stream's 256-column windows run a third of their lanes idle (measured: castle-size
         // images at B = 3-4 and 321 x 481 at B = 4-6 run faster as two rounds of tiles; 256 x 256 does not,
         // profiles/r03l_tile_threshold.txt)
         const long long ntiles = (long long)P * nb * tile_segs, cus = device_cus();
-        if (wg > 0 && (d->kernel_variant == 4 || ntiles <= cus || (tile_segs > 1 && ntiles <= 2 * cus))) {
+        const long long ntiles9 = (long long)P * nb9 * tile_segs;
+        if (wg > 0 && (d->kernel_variant == 4 || ntiles <= cus || (wg9 > 0 && ntiles9 <= cus) ||
+                       (tile_segs > 1 && ntiles <= 2 * cus))) {
             a.tile_r = 3;
+            a.tile_nw = 16;
             a.band_h = bh;
             a.nbands = nb;
+            // 72-row tiles (8 waves x 9 rows) when 48-row tiles would need a second round but these fit in one
+            if (ntiles > cus && wg9 > 0 && ntiles9 <= cus) {
+                a.tile_r = 9;
+                a.tile_nw = 8;
+                a.band_h = bh9;
+                a.nbands = nb9;
+            }
             // 32-row tiles (2 rows per wave) when they still fit in one round: one or a few images leave most
             // CUs idle at 48 rows (castle B = 1: 114 tiles of 48 rows vs 246 of 32 rows, 41.1 -> 35.0 us,
             // profiles/r03q_tile_r2_ab.txt); more tiles but shorter waves
             if (wg2 > 0 && (long long)P * nb2 * tile_segs <= cus) {
                 a.tile_r = 2;
+                a.tile_nw = 16;
                 a.band_h = bh2;
                 a.nbands = nb2;
             }

@@ -805,7 +805,9 @@ def test_auto_dispatch_by_shape():
                                                   (1, 50, 257, 1.0, 1e-5, 4), (1, 3, 321, 1.0, 1e-5, 10),
                                                   # enough tiles that 32-row tiles would need two rounds:
                                                   # 48-row tiles (3 rows per wave), plain and segmented
-                                                  (24, 100, 64, 1.0, 1e-5, 10), (24, 40, 301, 1.0, 3e-2, 10),
+                                                  (12, 100, 64, 1.0, 1e-5, 10), (24, 40, 301, 1.0, 3e-2, 10),
+                                                  # and 48-row tiles too: 72-row tiles (8 waves x 9 rows)
+                                                  (24, 100, 64, 1.0, 1e-5, 10), (24, 130, 64, 1.0, 3e-2, 10),
                                                   # one- and two-row images, one inner iteration
                                                   (2, 1, 40, 1.0, 1e-5, 10), (1, 2, 321, 1.0, 1e-5, 10),
                                                   (2, 37, 64, 1.0, 1e-5, 1)])
@@ -814,7 +816,8 @@ def test_tile_kernel_exact_vs_oracle(B, H, W, alpha, tol, n_tv):
     inline finalisation) in exact mode: samples, block means and TV state bit-identical to the CPU oracle
     for band cuts, narrow images (idle lanes), alpha != 1, deepinv's early stop and n_tv > 10; for rows
     padded to a pitch (W % 4 != 0) and column segments with n_tv halo columns (W > 256); 32-row tiles
-    where they fit on the CUs in one round, 48-row tiles for the larger batches."""
+    where they fit on the CUs in one round, 48-row tiles for the larger batches, 72-row tiles of 8 waves
+    where 48-row ones would need a second round."""
     from psgla_for_posterior_sampling_amd.engine import FusedTvChains
     from psgla_for_posterior_sampling_amd import hip_ops as K
     g = torch.Generator().manual_seed(9)
@@ -902,15 +905,15 @@ def test_tile_kernel_equals_stream_kernel_real_shapes(B, H, W):
             assert torch.equal(a, b), f"exact={exact}"
 
 
-@pytest.mark.parametrize("tol", [3e-3, 1e-3])
-def test_tile_kernel_early_stop_handoff_full_size(tol):
+@pytest.mark.parametrize("B,tol", [(8, 3e-3), (8, 1e-3), (16, 3e-3)])
+def test_tile_kernel_early_stop_handoff_full_size(B, tol):
     """The tile kernel's fence-free step hand-off (sc1 stores, rel-err sums as agent atomics read back by
     the last workgroup's agent atomics) under a tolerance at which deepinv's early stop fires: 40 steps of
-    8 chains at 3 x 256 x 256 bit-identical to the row-streaming kernel (which keeps its release / acquire
-    fences), and different from the same run without early stops (so stops did fire)."""
+    8 chains (48-row tiles) or 16 chains (72-row tiles) at 3 x 256 x 256 bit-identical to the row-streaming
+    kernel (which keeps its release / acquire fences), and different from the same run without early stops
+    (so stops did fire)."""
     from psgla_for_posterior_sampling_amd.engine import FusedTvChains
     from psgla_for_posterior_sampling_amd import hip_ops as K
-    B = 8
     g = torch.Generator(device=DEV).manual_seed(77)
     xs = torch.rand((B, 3, 256, 256), generator=g, device=DEV)
     gen = torch.Generator(device=DEV).manual_seed(0)
