@@ -774,7 +774,7 @@ def test_fused_single_channel_exact_vs_oracle(variant):
 
 def test_auto_dispatch_by_shape():
     """64 chains x 3 x 256 x 256 (BASELINE configs[1], one GPU): auto dispatch picks the row stream; 8 chains
-    (the 8-GPU strong split) the tile kernel; alpha != 1 and many chains of a real shape the row stream; one
+    (the 8-GPU strong split) and 16 (the 4-GPU split) the tile kernel; alpha != 1 and many chains of a real shape the row stream; one
     or two chains of a real shape (padded rows, column segments) the tile kernel."""
     from psgla_for_posterior_sampling_amd.engine import FusedTvChains
     from psgla_for_posterior_sampling_amd import hip_ops as K
@@ -792,7 +792,10 @@ def test_auto_dispatch_by_shape():
     assert kern(2, 321, 481) == "tv_tile_kernel"
     assert kern(4, 481, 321) == "tv_tile_kernel"        # two rounds of tiles beat segmented row streams
     assert kern(8, 481, 321) == "tv_stream_kernel"
-    assert kern(12, 256, 256) == "tv_stream_kernel"     # unsegmented rows: one round of tiles at most
+    # unsegmented rows: one round of tiles at most -- 72-row tiles (8 waves x 9 rows) where 48-row ones need two
+    assert kern(12, 256, 256) == "tv_tile_kernel"       # 36 planes x 5 bands
+    assert kern(16, 256, 256) == "tv_tile_kernel"       # the 4-GPU strong split: 48 planes x 5 bands
+    assert kern(20, 256, 256) == "tv_stream_kernel"     # 300 tiles of 72 rows: more than the CUs
 
 
 # ------------------------------------------------------------------------------ small-batch tile kernel

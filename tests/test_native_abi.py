@@ -83,7 +83,9 @@ def test_kernel_dispatch_rules_on_the_host():
 
     assert kind(64, 256, 256)[0] == STREAM                       # BASELINE configs[1], one GPU
     assert kind(8, 256, 256)[0] == TILE                          # 8-GPU strong split: 240 tiles
-    assert kind(12, 256, 256)[0] == STREAM                       # 360 tiles: two rounds lose to the stream
+    assert kind(12, 256, 256)[0] == TILE                         # 72-row tiles (8 waves x 9 rows): 180 tiles
+    assert kind(16, 256, 256)[0] == TILE                         # 4-GPU strong split: 240 tiles of 72 rows
+    assert kind(20, 256, 256)[0] == STREAM                       # 300 tiles of 72 rows: two rounds lose
     assert kind(64, 256, 256, alpha1=False)[0] == STREAM
     assert kind(1, 481, 321, ldw=324)[0] == TILE                 # castle at the CLI's batch 1
     assert kind(4, 481, 321, ldw=324)[0] == TILE                 # segmented rows: two rounds of tiles
