@@ -1474,9 +1474,11 @@ struct TileShared {
     int s_flag, s_item, s_next;
 };
 
-template <bool EXACT, bool ALPHA1, int R, bool GEN, int NW>
+// before_u2: called by every wave once the tile's rel-err sums and X side are issued, before its u2 stores
+// (the kernel's main pass: the step's arrival, so the u2 stores drain while the last workgroup finalises)
+template <bool EXACT, bool ALPHA1, int R, bool GEN, int NW, typename BeforeU2>
 __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, int plane, int seg, int band, int n_it,
-                                        bool track, long long step, bool fresh) {
+                                        bool track, long long step, bool fresh, BeforeU2&& before_u2) {
     float x2[R][CPL], u0[R][CPL], u1[R][CPL];
     double* const nrm = a.norms;
     const int lane = threadIdx.x & (WAVE - 1);
@@ -1765,6 +1767,7 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
     }
     // ---- 6. the core rows out: the X side (48-row tiles: issued before the last dual update), u2
     if (!EARLY_X || n_it <= 0) store_x_side();
+    before_u2();
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (!(rv[r] && core[r] && corelane)) continue;
@@ -1778,6 +1781,7 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
 template <bool EXACT, bool ALPHA1, int R, bool GEN, int NW>
 __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
     __shared__ TileShared<R, NW> sh;
+    constexpr bool SPLIT = NW == 8;                    // two-phase arrival (below)
     const long long step = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
     const bool fresh = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
     const int P = a.B * a.C;
@@ -1789,30 +1793,49 @@ __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
         const int N = P * T, per = (N + 7) / 8;
         const int x = blockIdx.x, xcd = x & 7, k = x >> 3;
         const int item = xcd * per + k;
-        if (item < N) {
-            const int plane = item / T, t = item - plane * T;
-            const int seg = GEN ? t / a.nbands : 0;
-            const int band = t - seg * a.nbands;
-            sb_tile<EXACT, ALPHA1, R, GEN, NW>(a, sh, plane, seg, band, a.n_tv, true, step, fresh);
-        }
-    }
-    if (!a.fin_inline) return;
-    // ---- step finalisation by the last workgroup to arrive (as tv_stream_kernel) ----
-    wait_vm0();
-    __syncthreads();
-    if (threadIdx.x == 0) {
+        // Arrival.  The 72-row tiles (SPLIT) arrive before their u2 stores, so those drain while the last
+        // workgroup finalises (16 chains 68.3 -> 67.0 us; the 16-wave tiles measured +1-1.4 % that way,
+        // profiles/r03s_tile_two_phase_ab.txt): the counter a.arrive then holds two counts, the low 16 bits
+        // the workgroups whose rel-err sums and X side are complete (phase 1: the last one finalises the
+        // step), the high bits those whose u2 stores are complete too (phase 2: the rare early-stop recompute
+        // rewrites outputs, so it waits for them); the last workgroup takes both counts out at the end, by
+        // one atomic add.  The other tiles arrive once everything is stored (phase 1 only).
+        auto arrive = [&]() {
+            if (!a.fin_inline) return;
+            wait_vm0();
+            __syncthreads();
+            if (threadIdx.x == 0) {
         // Without fences: every output of this kernel is an sc1 (write-through) store and every rel-err sum
         // an agent-scope atomic; each wave waited vmcnt(0) before the barrier above, one lane per workgroup
         // adds to the arrival counter, and the workgroup whose add returns the last count reads the sums by
         // agent atomics (MI355X_MICROARCH.md: "8-B agent atomics both sides" with its hand-off row 1; a
         // release + acquire pair cost 1.1 us per step here).  Nothing else this launch wrote is read by it
         // (the rare redo reads the step's inputs, written by the previous launch).
-        const int old = __hip_atomic_fetch_add(a.arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sh.s_flag = (old == (int)gridDim.x - 1) ? 1 : 0;
+                const int old = __hip_atomic_fetch_add(a.arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                sh.s_flag = ((old & 0xFFFF) == (int)gridDim.x - 1) ? 1 : 0;
+            }
+            wait_vm0();
+            __syncthreads();
+        };
+        if (item < N) {
+            const int plane = item / T, t = item - plane * T;
+            const int seg = GEN ? t / a.nbands : 0;
+            const int band = t - seg * a.nbands;
+            if constexpr (SPLIT) sb_tile<EXACT, ALPHA1, R, GEN, NW>(a, sh, plane, seg, band, a.n_tv, true, step, fresh, arrive);
+            else sb_tile<EXACT, ALPHA1, R, GEN, NW>(a, sh, plane, seg, band, a.n_tv, true, step, fresh, [] {});
+        }
+        if (!SPLIT || item >= N) arrive();
     }
-    wait_vm0();
-    __syncthreads();
-    if (!sh.s_flag) return;
+    if (!a.fin_inline) return;
+    if (!sh.s_flag) {
+        if (!SPLIT) return;
+        // phase 2: this workgroup's u2 stores are complete
+        wait_vm0();
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(a.arrive, 1 << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    // ---- step finalisation by the last workgroup to arrive (as tv_stream_kernel) ----
     const int G = a.B;
     for (int g = threadIdx.x; g < G; g += blockDim.x) sh.s_stop[g] = 0;
     __syncthreads();
@@ -1839,14 +1862,24 @@ __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
     }
     __syncthreads();
     if (sh.s_item) {
-        // rare: redo every tile of a stopped chain with the stopped iteration count (inputs intact)
+        // rare: redo every tile of a stopped chain with the stopped iteration count (inputs intact), once every
+        // other workgroup's stores are complete (phase 2; all of them have arrived, so each will count: bounded
+        // wait only as a guard)
+        if (SPLIT && threadIdx.x == 0) {
+            for (int spin = 0; spin < (1 << 24); ++spin) {
+                if ((__hip_atomic_load(a.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 16) >= (int)gridDim.x - 1) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        wait_vm0();
+        __syncthreads();
         for (int item = 0; item < P * T; ++item) {
             const int plane = item / T, t = item - plane * T;
             const int seg = GEN ? t / a.nbands : 0;
             const int band = t - seg * a.nbands;
             const int nstop = __builtin_amdgcn_readfirstlane(sh.s_stop[plane / a.C]);
             if (nstop < a.n_tv) {
-                sb_tile<EXACT, ALPHA1, R, GEN, NW>(a, sh, plane, seg, band, nstop, false, step, fresh);
+                sb_tile<EXACT, ALPHA1, R, GEN, NW>(a, sh, plane, seg, band, nstop, false, step, fresh, [] {});
                 wait_vm0();
                 __syncthreads();
             }
@@ -1855,7 +1888,11 @@ __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
     __syncthreads();
     for (int i = threadIdx.x; i < a.B * a.n_tv * 2; i += blockDim.x) a.norms[i] = 0.0;
     if (threadIdx.x == 0) {
-        *a.arrive = 0;
+        // both counts out (the other workgroups' phase-2 adds may still be landing: an add, not a store); the
+        // counter is 0 once the kernel has completed
+        const int G1 = (int)gridDim.x;
+        if (SPLIT) __hip_atomic_fetch_add(a.arrive, -(G1 + ((G1 - 1) << 16)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else *a.arrive = 0;
         if (a.fresh_dev) *a.fresh_dev = 0;
         if (a.advance_step && a.d_step) *a.d_step = step - a.step_offset + 1;   // the value read at the start: no dependent load
     }
@@ -2957,6 +2994,8 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
             TvArgs s = a;
             s.fin_inline = (mask & 2) ? 1 : 0;
             const int grid = ((P * s.nbands * s.st_nsegs + 7) / 8) * 8;   // tile_kernel: 8 runs of tiles
+            // (the two-phase arrival counter keeps a count of workgroups in 15 bits)
+            if (grid > 32767) return fail(0, "psgla_tv_step: more than 32767 tiles in one launch");
             const bool gen = !(s.ldw == s.W && s.st_nsegs == 1);
 #define PSGLA_TILE(NWV, RV)                                                                                        \
     if (s.tile_nw == NWV && s.tile_r == RV) {                                                                      \
