@@ -73,10 +73,11 @@ typedef struct PsglaSchedule {
  * is honoured, `fresh` is cleared and *d_step advanced once the step is complete.
  * What is launched depends on the variant the shape selects (kernel_variant 0):
  *   - the small-batch tile kernel (tv_tile_kernel: any W, rows padded to the pitch ldw and cut
- *     into the stream kernel's column segments when W > 256) when its 48-row tiles all fit on
- *     the CUs at once (few chains per GPU, or one / two real-size images): ONE launch; its last
- *     workgroup to finish evaluates the early stop, recomputes stopped chains and advances
- *     the step (no second kernel);
+ *     into the stream kernel's column segments when W > 256) when its 32-, 48- or 72-row tiles
+ *     all fit on the CUs at once (few chains per GPU, or a few real-size images; two rounds of
+ *     48-row tiles for segmented rows): ONE launch of at most 32767 tiles; its last workgroup
+ *     to arrive evaluates the early stop, recomputes stopped chains and advances the step (no
+ *     second kernel);
  *   - else the row-streaming kernel (tv_stream_kernel: row pitch ldw % 4 == 0,
  *     1 <= n_tv <= 10, H >= 2, every width with column segments, any alpha): one row per
  *     pipeline step, ONE launch, finalised in-kernel;
@@ -108,7 +109,8 @@ typedef struct PsglaTvStep {
     int32_t advance_step;     /* 1: finaliser increments *d_step                           */
     int32_t* fresh;           /* device int: 1 -> TV restart (x2=Y, u2=0), cleared after the step */
     double* norms;            /* device [B][n_tv][2], zero-initialised (rel_err partial sums) */
-    int32_t* arrive;          /* device int, zero-initialised (finaliser arrival counter)   */
+    int32_t* arrive;          /* device int, zero-initialised (finaliser arrival counter; zero
+                                 again once each step's launch has completed)                */
     int32_t launch_mask;      /* 0 or 3: both kernels; 1: tile kernel only (re-runs the same step:
                                  idempotent, for kernel timing); 2: finaliser only            */
     int32_t kernel_variant;   /* 0: auto (see above); 1: force the band kernel; 2: force the row stream
