@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PSGLA_HIP_ABI_VERSION 7
+#define PSGLA_HIP_ABI_VERSION 8
 
 /* Max inner TV iterations the fused (temporally blocked) kernel handles. */
 #define PSGLA_TV_MAX_FUSED_IT 24
@@ -126,6 +126,10 @@ typedef struct PsglaTvStep {
                                  images run on the streaming / tile kernels) needs one of them;
                                  the padding columns are scratch (never read into the image).
                                  The noise stream is indexed by the unpadded element.            */
+    int32_t norms_copies;     /* (ABI 8) 0 or 1: norms is [B][n_tv][2]; K > 1: norms holds K zero-initialised
+                                 copies [K][B][n_tv][2] and the tile kernel spreads its workgroups'
+                                 rel-err partial sums over them (workgroup x adds to copy x % K), so
+                                 that many tiles of one chain do not queue on the same atomics   */
 } PsglaTvStep;
 
 int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream);

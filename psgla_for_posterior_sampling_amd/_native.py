@@ -11,7 +11,7 @@ import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PSGLA_LIB", os.path.join(_PKG, "libpsgla_hip.so"))
-ABI_VERSION = 7
+ABI_VERSION = 8
 TV_MAX_FUSED_IT = 24
 
 
@@ -45,7 +45,7 @@ class PsglaTvStep(ctypes.Structure):
         ("tau", c_f), ("one_plus_tau", c_f), ("sigma_tv", c_f), ("rho", c_f), ("ths", c_f), ("tol", c_f),
         ("n_tv", c_i32), ("exact", c_i32), ("seed", c_u64), ("chain0", c_i32), ("advance_step", c_i32),
         ("fresh", c_vp), ("norms", c_vp), ("arrive", c_vp), ("launch_mask", c_i32),
-        ("kernel_variant", c_i32), ("stream_wgs", c_i32), ("ldw", c_i32),
+        ("kernel_variant", c_i32), ("stream_wgs", c_i32), ("ldw", c_i32), ("norms_copies", c_i32),
     ]
 
 

@@ -98,6 +98,7 @@ struct TvArgs {
     int fin_inline;                 // stream kernel: 1 = the last workgroup finalises the step
     int tile_r;                     // > 0: small-batch tile kernel with tile_r rows per wave (one tile per workgroup)
     int tile_nw;                    // tile kernel: waves per workgroup (16 or 8)
+    int norm_copies;                // tile kernel: copies of norms its rel-err sums are spread over (>= 1)
 };
 
 // Inner iterations (chunk-local) whose rel_err deepinv tests: global index >= 2 ("it > 1"); in the call's
@@ -1761,8 +1762,11 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
             for (int ww = 0; ww < NW; ++ww)
                 for (int q = 0; q < 4; ++q) { sd += sh.red[t][ww][q].x; sn += sh.red[t][ww][q].y; }
             if (!EXACT) sd *= (double)(a.rho * a.rho);     // fast sums hold (x - x2_prev)^2
-            atomicAdd(&nrm[((size_t)b * a.n_tv + t) * 2], sd);
-            atomicAdd(&nrm[((size_t)b * a.n_tv + t) * 2 + 1], sn);
+            // workgroup x adds to copy x % norm_copies (x & 7 = its XCD when there are 8): fewer adds queue
+            // on one address when many tiles share a chain
+            double* const nc = nrm + (size_t)(blockIdx.x % a.norm_copies) * ((size_t)a.B * a.n_tv * 2);
+            atomicAdd(&nc[((size_t)b * a.n_tv + t) * 2], sd);
+            atomicAdd(&nc[((size_t)b * a.n_tv + t) * 2 + 1], sn);
         }
     }
     // ---- 6. the core rows out: the X side (48-row tiles: issued before the last dual update), u2
@@ -1844,10 +1848,14 @@ __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
         if (t >= trk_lo(a) && t <= trk_hi(a) && t < a.n_tv) {
             // read by agent-scope atomics (+0.0, returning), as they were written: 8-B agent atomics on both
             // sides of the hand-off, performed where the producers' adds were
-            const double nd = __hip_atomic_fetch_add(&a.norms[((size_t)g * a.n_tv + t) * 2], 0.0, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-            const double nn = __hip_atomic_fetch_add(&a.norms[((size_t)g * a.n_tv + t) * 2 + 1], 0.0, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
+            double nd = 0.0, nn = 0.0;
+            for (int cp = 0; cp < a.norm_copies; ++cp) {   // the copies in a fixed order
+                double* const nc = a.norms + (size_t)cp * ((size_t)a.B * a.n_tv * 2);
+                nd += __hip_atomic_fetch_add(&nc[((size_t)g * a.n_tv + t) * 2], 0.0, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+                nn += __hip_atomic_fetch_add(&nc[((size_t)g * a.n_tv + t) * 2 + 1], 0.0, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+            }
             const float rel = (float)sqrt(nd) / (float)sqrt(nn);
             if (rel < a.tol) atomicOr(&sh.s_stop[g], 1 << t);
         }
@@ -1886,7 +1894,7 @@ __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < a.B * a.n_tv * 2; i += blockDim.x) a.norms[i] = 0.0;
+    for (int i = threadIdx.x; i < a.B * a.n_tv * 2 * a.norm_copies; i += blockDim.x) a.norms[i] = 0.0;
     if (threadIdx.x == 0) {
         // both counts out (the other workgroups' phase-2 adds may still be landing: an add, not a store); the
         // counter is 0 once the kernel has completed
@@ -2996,6 +3004,10 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
             const int grid = ((P * s.nbands * s.st_nsegs + 7) / 8) * 8;   // tile_kernel: 8 runs of tiles
             // (the two-phase arrival counter keeps a count of workgroups in 15 bits)
             if (grid > 32767) return fail(0, "psgla_tv_step: more than 32767 tiles in one launch");
+            // several copies of the rel-err sums only where many tiles share a chain (castle at B = 1: 246 tiles,
+            // 34.8 -> 33.0 us); with 15-66 tiles per chain the last workgroup's reads of 8 copies cost more
+            // (+4-5 %) than the queueing they save (profiles/r03s_tile_norm_copies_ab.txt)
+            if (s.norm_copies < 1 || s.C * s.nbands * s.st_nsegs < 128) s.norm_copies = 1;
             const bool gen = !(s.ldw == s.W && s.st_nsegs == 1);
 #define PSGLA_TILE(NWV, RV)                                                                                        \
     if (s.tile_nw == NWV && s.tile_r == RV) {                                                                      \
@@ -3163,6 +3175,7 @@ int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream) {
     a.n_tv = d->n_tv; a.seed = d->seed; a.chain0 = d->chain0; a.pingpong = 1;
     a.d_step = (long long*)s->d_step; a.step_offset = s->step_offset;
     a.fresh_dev = d->fresh; a.per_chain_norm = 1; a.norms = d->norms; a.arrive = d->arrive;
+    a.norm_copies = d->norms_copies > 1 ? d->norms_copies : 1;
     a.it0 = 0; a.last_chunk = 1; a.stopped = nullptr;
     a.advance_step = d->advance_step;
     a.n_inter = s->n_inter; a.nm = s->n_inter_mmse; a.coef = s->acc_coef;

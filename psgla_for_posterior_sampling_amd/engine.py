@@ -63,7 +63,9 @@ class FusedTvChains:
         self.y = self._padded(y)
         self.mask = self._padded(mask_u8)
         self.sched = K.Schedule(self.pshape, n_iter, n_inter, n_inter_mmse, dev, store_samples, store_blocks)
-        self.work = K.TvWorkspace(B, tv.n_it, dev)
+        # rel-err partial sums spread over 8 copies (one per XCD) for the tile kernel: one image's 246 tiles
+        # no longer queue on the same 16 atomics (castle B = 1: DESIGN.md 3.1b)
+        self.work = K.TvWorkspace(B, tv.n_it, dev, copies=8)
         self.work.fresh.fill_(0 if warm else 1)
         self.steps_done = 0
         self.n_iter = int(n_iter)
@@ -92,7 +94,8 @@ class FusedTvChains:
         d.chain0 = int(chain0)
         d.advance_step = 1
         d.fresh = self.work.fresh.data_ptr()
-        d.norms = self.work.norms.data_ptr()
+        d.norms = self.work.norms_all.data_ptr()
+        d.norms_copies = self.work.copies
         d.arrive = self.work.arrive.data_ptr()
         d.kernel_variant = KERNEL_VARIANTS[kernel_variant]
         d.stream_wgs = int(stream_wgs)

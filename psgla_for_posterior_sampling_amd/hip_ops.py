@@ -347,9 +347,13 @@ def tv_prox(y: torch.Tensor, ths: float, k: TvConstants, x2_in=None, u2_in=None,
 
 
 class TvWorkspace:
-    """Zero-initialised early-stop workspace: norms[groups][n_it][2] (fp64) + arrival counter."""
+    """Zero-initialised early-stop workspace: norms[groups][n_it][2] (fp64) + arrival counter.  copies > 1:
+    norms_all holds that many such arrays back to back (PsglaTvStep.norms_copies), `norms` is the first."""
 
-    def __init__(self, groups: int, n_it: int, device):
-        self.norms = torch.zeros((max(groups, 1), max(n_it, 1), 2), dtype=torch.float64, device=device)
+    def __init__(self, groups: int, n_it: int, device, copies: int = 1):
+        self.copies = max(int(copies), 1)
+        self.norms_all = torch.zeros((self.copies * max(groups, 1), max(n_it, 1), 2), dtype=torch.float64,
+                                     device=device)
+        self.norms = self.norms_all[:max(groups, 1)]
         self.arrive = torch.zeros(4, dtype=torch.int32, device=device)
         self.fresh = torch.zeros(4, dtype=torch.int32, device=device)
