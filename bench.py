@@ -306,6 +306,17 @@ def main():
     blocks, _ = eng.blocks()
     psnr_sum, n_chains = reduce_psnr(blocks, xs, world)
 
+    # ---- placement: every rank's device and PCI address, gathered to rank 0 (small metadata) ----
+    props = torch.cuda.get_device_properties(dev)
+    here = {"rank": rank, "local_rank": local, "device": torch.cuda.current_device(),
+            "pci": f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}",
+            "chains": [c0, c1]}
+    placement = [here]
+    if world > 1:
+        import torch.distributed as dist
+        placement = [None] * world
+        dist.all_gather_object(placement, here)
+
     traffic, traffic_info = None, None
     kname = eng.main_kernel            # the kernel the timed graphs launch, once per step
     pmc_json = args.pmc_json or os.path.join(REPO, PMC_PROFILES.get(kname, "none"))
@@ -357,6 +368,9 @@ def main():
             "cpu_baseline": cpu,
             "mmse_psnr_mean_db": round(psnr_sum / max(n_chains, 1), 3),
         }
+        if world > 1:
+            line["config"]["placement"] = placement
+            line["config"]["distinct_gpus"] = len({p["pci"] for p in placement})
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PSGLA_HIP_ABI_VERSION 8
+#define PSGLA_HIP_ABI_VERSION 9
 
 /* Max inner TV iterations the fused (temporally blocked) kernel handles. */
 #define PSGLA_TV_MAX_FUSED_IT 24
@@ -109,8 +109,11 @@ typedef struct PsglaTvStep {
     int32_t advance_step;     /* 1: finaliser increments *d_step                           */
     int32_t* fresh;           /* device int: 1 -> TV restart (x2=Y, u2=0), cleared after the step */
     double* norms;            /* device [B][n_tv][2], zero-initialised (rel_err partial sums) */
-    int32_t* arrive;          /* device int, zero-initialised (finaliser arrival counter; zero
-                                 again once each step's launch has completed)                */
+    int32_t* arrive;          /* device int[4], zero-initialised: [0] finaliser arrival counter (zero
+                                 again once each step's launch has completed); [3] (ABI 9) set to 1
+                                 if the tile kernel's early-stop recompute ever stopped waiting for
+                                 the other workgroups' stores (a guard that should never expire:
+                                 the host checks it, FusedTvChains.check_handoff)               */
     int32_t launch_mask;      /* 0 or 3: both kernels; 1: tile kernel only (re-runs the same step:
                                  idempotent, for kernel timing); 2: finaliser only            */
     int32_t kernel_variant;   /* 0: auto (see above); 1: force the band kernel; 2: force the row stream

@@ -11,7 +11,7 @@ import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PSGLA_LIB", os.path.join(_PKG, "libpsgla_hip.so"))
-ABI_VERSION = 8
+ABI_VERSION = 9
 TV_MAX_FUSED_IT = 24
 
 

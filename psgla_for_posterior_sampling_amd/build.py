@@ -1,25 +1,37 @@
 """In-tree build of libpsgla_hip.so (gfx950).  Used by ``__graft_entry__.build()``.
 
-    hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared -I include \
-          -o psgla_for_posterior_sampling_amd/libpsgla_hip.so csrc/psgla_kernels.hip
+One translation unit per kernel family (csrc/*.hip), compiled in parallel, then linked:
+
+    hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -fPIC -I include \
+          -c csrc/<unit>.hip -o build/<unit>.o          (one process per unit)
+    hipcc -shared -fPIC -o psgla_for_posterior_sampling_amd/libpsgla_hip.so build/*.o
 
 -fno-slp-vectorize: packed fp32 (v_pk_*) needs operand shuffles and measured slower on gfx950.
 -ffp-contract=off keeps the reference's separate multiply/add roundings (the EXACT
 kernels are bit-identical to the torch CPU checker); fmas are written explicitly
 where the fast kernels want them.
+
+Diagnostic variants (tools/variant_build.py) rebuild only the units their patches touch.
 """
 from __future__ import annotations
 
+import glob
 import os
 import shutil
 import subprocess
+from concurrent.futures import ThreadPoolExecutor
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
-SOURCES = [os.path.join(PKG, "csrc", "psgla_kernels.hip")]
-HEADERS = [os.path.join(PKG, "csrc", "noise.hpp"), os.path.join(REPO, "include", "psgla_hip.h")]
+CSRC = os.path.join(PKG, "csrc")
+UNITS = ["api", "tv_stream", "tv_tile", "tv_band", "blur", "elementwise"]
+SOURCES = [os.path.join(CSRC, u + ".hip") for u in UNITS]
+HEADERS = [os.path.join(CSRC, "noise.hpp"), os.path.join(CSRC, "psgla_common.hpp"),
+           os.path.join(REPO, "include", "psgla_hip.h")]
 OUT = os.path.join(PKG, "libpsgla_hip.so")
+OBJ = os.path.join(REPO, "build", "obj")
 ARCH = os.environ.get("PSGLA_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-Wno-inline-asm", "-fPIC"]
 
 
 def hipcc() -> str:
@@ -36,18 +48,43 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(s) <= t for s in SOURCES + HEADERS)
 
 
-def build_native(force: bool = False, verbose: bool = False, out: str = OUT) -> str:
-    if not force and out == OUT and up_to_date():
-        return OUT
-    extra = os.environ.get("PSGLA_HIPCC_EXTRA", "").split()
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-Wno-inline-asm", "-fPIC",
-           "-shared", "-I", os.path.join(REPO, "include"), "-o", out + ".tmp"] + extra + SOURCES
+def compile_units(sources, objdir, extra=(), include=(), verbose=False):
+    """Compile each source to objdir/<name>.o in parallel; returns the object paths."""
+    os.makedirs(objdir, exist_ok=True)
+    inc = ["-I", os.path.join(REPO, "include"), "-I", CSRC]
+    for d in include:
+        inc += ["-I", d]
+
+    def one(src):
+        obj = os.path.join(objdir, os.path.splitext(os.path.basename(src))[0] + ".o")
+        cmd = [hipcc(), f"--offload-arch={ARCH}"] + FLAGS + list(extra) + inc + ["-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        return obj
+
+    jobs = min(len(sources), max(1, int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        return list(ex.map(one, sources))
+
+
+def link(objs, out, verbose=False):
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + list(objs)
     if verbose:
-        print(" ".join(cmd))
+        print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
     return out
 
 
+def build_native(force: bool = False, verbose: bool = False, out: str = OUT) -> str:
+    if not force and out == OUT and up_to_date():
+        return OUT
+    extra = os.environ.get("PSGLA_HIPCC_EXTRA", "").split()
+    objs = compile_units(SOURCES, OBJ, extra=extra, verbose=verbose)
+    return link(objs, out, verbose=verbose)
+
+
 if __name__ == "__main__":
     print(build_native(force=True, verbose=True))
+    print("units:", sorted(os.path.basename(p) for p in glob.glob(os.path.join(OBJ, "*.o"))))

@@ -230,6 +230,14 @@ class FusedTvChains:
             n -= reps * graph_steps
         self.step(n)
 
+    def check_handoff(self):
+        """Raise if the tile kernel's early-stop recompute ever gave up waiting for the other workgroups'
+        stores (arrive[3], include/psgla_hip.h; a guard that should never expire -- if it did, the
+        recomputed chains may have been overwritten by late first-pass stores).  One host sync."""
+        if int(self.work.arrive[3].item()) != 0:
+            raise RuntimeError("tv_tile_kernel: early-stop recompute hand-off guard expired; results of the "
+                               "recomputed chains are not trustworthy")
+
     # -- results --------------------------------------------------------------------
     @property
     def X(self) -> torch.Tensor:

@@ -156,6 +156,7 @@ def psgla(init, data_grad, denoiser, alpha, lambd, sig_float=0.0055, delta=4e-5,
                                        c1, c2, seed, chain0, i)
                 snaps.save(i, eng.X, Yi, eng.lists())
             _run_with_snapshots(run_fused, n_iter, Kfreq, snap)
+        eng.check_handoff()
         denoiser.x2 = eng.x2_state.contiguous().clone()
         denoiser.u2 = eng.u2_state.contiguous().clone()
         denoiser.restart = False

@@ -321,11 +321,21 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo")          # per-image records only: no collective on the hot path
     ndev = max(torch.cuda.device_count(), 1)
     device = torch.device("cuda:" + str((pars.gpu_number + local) % ndev))
+    obj_group = None
+    if world > 1:
+        # no collective on the hot path: the per-image results are gathered once at the end -- their arrays over
+        # RCCL (device tensors) when every rank has a GPU of its own, the small metadata over a gloo group
+        import torch.distributed as dist
+        from .sharding import dist_backend
+        backend = dist_backend(int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
+        if backend == "nccl":
+            torch.cuda.set_device(device)
+            dist.init_process_group("nccl", device_id=device)
+            obj_group = dist.new_group(backend="gloo")
+        else:
+            dist.init_process_group(backend)
     sequential = world == 1 and pars.batch_size == 1
     if pars.save_images_online and not sequential:
         raise ValueError("--save_images_online needs a sequential run (--batch_size 1, one rank)")
@@ -359,22 +369,20 @@ def main(argv=None):
         for i, (record, _extras, mask, name) in zip(batch, restore_batch(pars, argv, ims, ids[batch[0]], denoiser,
                                                                            device)):
             local_out[i] = (record, None if mask is None else mask.cpu(), name)
-    if world > 1:
-        import torch.distributed as dist
-        parts = [None] * world
-        dist.all_gather_object(parts, local_out)
-        gathered = {}
-        for d in parts:
-            gathered.update(d)
-    else:
-        gathered = local_out
+    from .sharding import gather_records, reduce_dataset_psnr
+    psnr_sum, ssim_sum, n_img = reduce_dataset_psnr(local_out, world, device)
+    gathered = gather_records(local_out, world, rank, device, obj_group)
     records = []
     if rank == 0:
         for i in indices:
             record, mask, name = gathered[i]
             write_result(pars, os.path.join(path_result, "im_" + str(i)), name, record, mask)
             records.append(record)
+        if n_img:
+            print("Dataset ({} images): mean output PSNR {:.2f} dB / mean output SSIM {:.2f}".format(
+                n_img, psnr_sum / n_img, ssim_sum / n_img))
     if world > 1:
+        import torch.distributed as dist
         dist.barrier()
         dist.destroy_process_group()
     return records

@@ -45,7 +45,7 @@ def test_denoiser_prior_matches_reference_closure():
 
 def test_drunet_size_dispatch_follows_deepinv():
     """deepinv 0.2.1 DRUNet.forward's routes (KAIR utils_model): forward_unet in eval mode for sides
-    % 8 == 0 and > 31, test_pad in training mode or(modulo 16) when a side is < 32, test_onesplit(refield 64) otherwise.  With an
+    % 8 == 0 and > 31, test_pad(modulo 16) in training mode or when a side is < 32, test_onesplit(refield 64) otherwise.  With an
     elementwise stand-in for the U-Net every route returns exactly 2 x its input (the stitching is
     checked pixel for pixel); the recorded input shapes name the route."""
     m = DRUNet(nc=(8, 16, 32, 64), nb=1)

@@ -1,5 +1,6 @@
 """End-to-end CLI run (sampling_images.py surface) on a tiny synthetic dataset, on the GPU."""
 import os
+import socket
 
 import numpy as np
 import pytest
@@ -85,8 +86,12 @@ def test_bench_multirank_rehearsal():
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     base = ["bench.py", "--steps", "20", "--warmup", "5", "--no-cpu", "--kernel-iters", "3", "--warmup-seconds", "0"]
     env = dict(os.environ, PSGLA_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
     two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                          "--master-addr", "127.0.0.1", "--master-port", "29533"] + base + ["--gpus", "2"],
+                          "--master-addr", "127.0.0.1", "--master-port", str(port)] + base + ["--gpus", "2"],
                          cwd=repo, env=env, capture_output=True, text=True, timeout=240)
     assert two.returncode == 0, two.stderr[-2000:]
     d2 = json.loads([l for l in two.stdout.splitlines() if l.startswith("{")][-1])
@@ -96,6 +101,10 @@ def test_bench_multirank_rehearsal():
     assert d2["n_gpus"] == 2 and d2["config"]["chains_per_gpu"] == 32 and d2["config"]["global_batch"] == 64
     assert d2["scaling"] == "strong" and d2["value"] > 0
     assert abs(d2["mmse_psnr_mean_db"] - d1["mmse_psnr_mean_db"]) < 1e-9
+    # the N > 1 line names every rank's device and PCI address (one GPU here: both ranks on it)
+    pl = d2["config"]["placement"]
+    assert [p["rank"] for p in pl] == [0, 1] and [p["chains"] for p in pl] == [[0, 32], [32, 64]]
+    assert d2["config"]["distinct_gpus"] == len({p["pci"] for p in pl}) == 1
 
 
 def _two_shape_dataset(root):
@@ -159,12 +168,18 @@ def test_cli_batched_and_sharded_equal_sequential(tmp_path, den):
         runs[tag] = _records(str(tmp_path / tag), 5)
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", PYTHONPATH=repo)
+    env.pop("PSGLA_DIST_BACKEND", None)   # the CLI's own choice: gloo here (two ranks, one GPU), nccl on a node
+    sock = socket.socket()                # a free port, not a fixed one a leftover rendezvous may still hold
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
     two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                          "--master-addr", "127.0.0.1", "--master-port", "29541", "-m",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), "-m",
                           "psgla_for_posterior_sampling_amd.sampling_images"] + common
                          + ["--results_root", str(tmp_path / "ranks"), "--batch_size", "4"],
                          cwd=repo, env=env, capture_output=True, text=True, timeout=300)
     assert two.returncode == 0, two.stderr[-3000:]
+    assert "Dataset (5 images): mean output PSNR" in two.stdout, two.stdout[-2000:]
     runs["ranks"] = _records(str(tmp_path / "ranks"), 5)
     # TV (the HIP step alone) is bit-identical; DnCNN's forward runs on MIOpen, whose convolution solver is
     # chosen per batch size (B = 1, 2, 3 here), so its records agree to fp32 rounding (measured 6e-7 rel.)

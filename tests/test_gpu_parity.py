@@ -908,19 +908,23 @@ def test_tile_kernel_equals_stream_kernel_real_shapes(B, H, W):
             assert torch.equal(a, b), f"exact={exact}"
 
 
-@pytest.mark.parametrize("B,tol", [(8, 3e-3), (8, 1e-3), (16, 3e-3)])
-def test_tile_kernel_early_stop_handoff_full_size(B, tol):
+@pytest.mark.parametrize("B,H,W,tol", [(8, 256, 256, 3e-3), (8, 256, 256, 1e-3), (16, 256, 256, 3e-3),
+                                       (1, 481, 321, 3e-3), (2, 321, 481, 3e-3)])
+def test_tile_kernel_early_stop_handoff_full_size(B, H, W, tol):
     """The tile kernel's fence-free step hand-off (sc1 stores, rel-err sums as agent atomics read back by
     the last workgroup's agent atomics) under a tolerance at which deepinv's early stop fires: 40 steps of
-    8 chains (48-row tiles) or 16 chains (72-row tiles) at 3 x 256 x 256 bit-identical to the row-streaming
-    kernel (which keeps its release / acquire fences), and different from the same run without early stops
-    (so stops did fire)."""
+    8 chains (48-row tiles) or 16 chains (72-row tiles) at 3 x 256 x 256, and the reference's real shapes at
+    the CLI's batch sizes (castle 481 x 321 at B = 1, 321 x 481 at B = 2: >= 128 tiles per chain, so the
+    rel-err sums are spread over the workspace's 8 norm copies, ABI 8), bit-identical to the row-streaming
+    kernel (which keeps its release / acquire fences and one norm copy), and different from the same run
+    without early stops (so stops did fire).  After every run the whole norms workspace (all copies) is
+    zero again: the finaliser summed and cleared every copy."""
     from psgla_for_posterior_sampling_amd.engine import FusedTvChains
     from psgla_for_posterior_sampling_amd import hip_ops as K
     g = torch.Generator(device=DEV).manual_seed(77)
-    xs = torch.rand((B, 3, 256, 256), generator=g, device=DEV)
+    xs = torch.rand((B, 3, H, W), generator=g, device=DEV)
     gen = torch.Generator(device=DEV).manual_seed(0)
-    mask2d = (torch.rand((256, 256), generator=gen, device=DEV) > 0.5).to(torch.uint8)
+    mask2d = (torch.rand((H, W), generator=gen, device=DEV) > 0.5).to(torch.uint8)
     y = mask2d.float() * xs + torch.normal(torch.zeros_like(xs), std=(1 / 255.0) * torch.ones_like(xs),
                                            generator=gen)
     init = (mask2d.float() * y + (1 - mask2d.float()) * 0.5).contiguous()
@@ -930,8 +934,13 @@ def test_tile_kernel_early_stop_handoff_full_size(B, tol):
         eng = FusedTvChains(init, y.contiguous(), mask2d, c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
                             alpha=1.0, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10, tol=t),
                             seed=0, n_iter=40, n_inter=10, n_inter_mmse=10, kernel_variant=variant)
+        assert eng.main_kernel == "tv_" + variant + "_kernel"
         eng.run(40, graph_steps=10)
         torch.cuda.synchronize()
+        assert eng.work.copies == 8
+        assert not torch.any(eng.work.norms_all != 0).item(), "norm copies left non-zero after a step"
+        assert int(eng.work.arrive[0].item()) == 0, "arrival counter not reset"
+        eng.check_handoff()
         bm, bm2 = eng.blocks()
         outs[(variant, t)] = (eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone())
     for a, b in zip(outs[("stream", tol)], outs[("tile", tol)]):

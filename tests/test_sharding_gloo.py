@@ -89,3 +89,70 @@ def test_two_rank_sharding_matches_single_process(tmp_path):
         assert abs(got["psnr_sum"] - ref_psnr) < 1e-9 * max(1.0, abs(ref_psnr))
         assert torch.equal(got["last"], last)        # bit-identical per chain, any split
         assert torch.equal(got["gt"], gt)
+
+
+def _fake_record(i):
+    """A result record shaped like metrics.analyse_run's + the run parameters (sampling_images.py:409-470)."""
+    import numpy as np
+    rng = np.random.default_rng(100 + i)
+    h, w = (6, 5) if i % 2 else (5, 7)                 # two image shapes, as CBSD68's two orientations
+    rec = {"PSNR_sample": [float(v) for v in rng.normal(20, 1, 4)], "SIM_sample": [float(v) for v in rng.random(4)],
+           "PSNR_mmse": [float(v) for v in rng.normal(25, 1, 3)], "SIM_list": [],
+           "observation": rng.random((h, w, 3), dtype=np.float32), "init": rng.random((h, w, 3), dtype=np.float32),
+           "PSNR_y": float(rng.normal(8, 1)), "SIM_y": 0.1 * i, "ground_truth": rng.random((h, w, 3), dtype=np.float32),
+           "MMSE": rng.random((h, w, 3), dtype=np.float32), "PSNR_MMSE": 27.0 + i, "SIM_MMSE": 0.8,
+           "std": rng.random((h, w, 3)).astype(np.float32), "diff": rng.random((h, w, 3)),   # float64 too
+           "n_iter": 1000, "s": 10 / 255.0, "alpha": 1.0, "sigma": 1.0, "l": 4, "lambda": 10.0, "delta": 1.5e-3}
+    mask = torch.from_numpy(rng.random((1, 3, h, w)) > 0.5).to(torch.int64)
+    return rec, mask, f"sigma1.0_s10_{i}"
+
+
+N_IMAGES = 5
+
+
+def _records_worker(rank, world, port, out_dir):
+    from psgla_for_posterior_sampling_amd.sharding import gather_records, reduce_dataset_psnr
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        a, b = chain_range(N_IMAGES, world, rank)
+        local = {i: _fake_record(i) for i in range(a, b)}
+        s, q, n = reduce_dataset_psnr(local, world, "cpu")
+        got = gather_records(local, world, rank, "cpu")
+        torch.save({"sum": s, "n": n, "none": got is None}, os.path.join(out_dir, f"s{rank}.pt"))
+        if rank == 0:
+            import pickle
+            with open(os.path.join(out_dir, "records.pkl"), "wb") as f:   # written and read by this test only
+                pickle.dump(got, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_records_gather_exact(tmp_path):
+    """The sharded CLI's result path (sampling_images.main, world > 1): per-image records gathered to rank 0
+    through one float64 tensor per rank plus gather_object metadata -- every array, list, scalar, dtype and
+    the mask come back identical; the dataset PSNR all_reduce counts every image once; other ranks get None."""
+    import pickle
+    import numpy as np
+    world = 2
+    mp.start_processes(_records_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    with open(os.path.join(tmp_path, "records.pkl"), "rb") as f:
+        got = pickle.load(f)
+    assert sorted(got) == list(range(N_IMAGES))
+    for i in range(N_IMAGES):
+        rec, mask, name = _fake_record(i)
+        grec, gmask, gname = got[i]
+        assert gname == name and set(grec) == set(rec)
+        for k, v in rec.items():
+            if isinstance(v, np.ndarray):
+                assert grec[k].dtype == v.dtype and np.array_equal(grec[k], v), k
+            else:
+                assert type(grec[k]) is type(v) and grec[k] == v, k
+        assert gmask.dtype == mask.dtype and torch.equal(gmask, mask)
+    for r in range(world):
+        s = torch.load(os.path.join(tmp_path, f"s{r}.pt"), weights_only=True)
+        assert s["n"] == N_IMAGES
+        assert abs(s["sum"] - sum(27.0 + i for i in range(N_IMAGES))) < 1e-9
+        assert s["none"] == (r != 0)
