@@ -27,17 +27,34 @@ namespace psgla {
 // ---------------------------------------------------------------------------------------
 
 
-struct StreamShared {
-    float4 x2[SP_MAXST + 1][2][WAVE];     // ring k = output of stage k (k = 0: front), 2 row slots
-    float4 u0[SP_MAXST + 1][2][WAVE];
-    float4 u1[SP_MAXST + 1][2][WAVE];
+// LDS of a workgroup.  Rings hold (x2, u2) rows between stages, u2 in its memory layout: two float4 per lane,
+// (u0, u1) of the lane's columns 0-1 (ua) and 2-3 (ub).  A1 (alpha == 1, the benched case): stage 1 reads its
+// TV input (x2 = X, u2) straight from the front's LDS-DMA staging -- no ring 0 copy by the front -- so those
+// staging parts are triple-buffered (a row's slot is re-targeted by the DMA of the row 12 later, issued after
+// stage 1 has read it); the observation y and the mask stay double-buffered (only the front reads them).
+// !A1: the front's staging (X, y, u2 lo / hi, x2) is double-buffered and the front writes ring 0.
+template <bool A1>
+struct StreamSharedT {
+    static constexpr int NR = SP_MAXST + (A1 ? 0 : 1);   // rings: stage outputs (+ ring 0 = the front's, !A1)
+    float4 x2[NR][2][WAVE];
+    float4 ua[NR][2][WAVE];
+    float4 ub[NR][2][WAVE];
     float4 y[SP_YRING][WAVE];             // Y rows (prox anchor), alive from the front to the back
-    // LDS-DMA staging (global_load_lds_dwordx4): a front wave's next row (X, y, u2 lo/hi, x2)
-    // and a back wave's next mean/sq rows land here without occupying VGPRs.
-    float4 fst[SP_FRONT][2][5][WAVE];
+    // LDS-DMA staging (global_load_lds_dwordx4): a front wave's next rows and a back wave's next mean / sq rows
+    // land here without occupying VGPRs.  A1: fsx[fw][row slot (q / 4) % 3][X, u2 lo, u2 hi], fsy[fw][(q / 4) % 2]
+    // = y; !A1: fsx[fw][(q / 4) % 2][X, y, u2 lo, u2 hi, x2].
+    float4 fsx[SP_FRONT][A1 ? 3 : 2][A1 ? 3 : 5][WAVE];
+    float4 fsy[SP_FRONT][A1 ? 2 : 1][WAVE];
     uint32_t fmk[SP_FRONT][2][WAVE];
     float4 bst[SP_BACK][2][2][WAVE];
     float red[SP_MAXSEG][SP_MAXST][2];
+    // ring holding the output of stage k (k = 0: the front's ring 0, !A1 only)
+    static __device__ __forceinline__ constexpr int rk(int k) { return A1 ? k - 1 : k; }
+    __device__ __forceinline__ float4* stX(int fw, int q) { return A1 ? &fsx[fw][((q >> 2) % 3)][0][0] : &fsx[fw][(q >> 2) & 1][0][0]; }
+    __device__ __forceinline__ float4* stY(int fw, int q) { return A1 ? &fsy[fw][(q >> 2) & 1][0] : &fsx[fw][(q >> 2) & 1][1][0]; }
+    __device__ __forceinline__ float4* stUa(int fw, int q) { return A1 ? &fsx[fw][((q >> 2) % 3)][1][0] : &fsx[fw][(q >> 2) & 1][2][0]; }
+    __device__ __forceinline__ float4* stUb(int fw, int q) { return A1 ? &fsx[fw][((q >> 2) % 3)][2][0] : &fsx[fw][(q >> 2) & 1][3][0]; }
+    __device__ __forceinline__ float4* stX2(int fw, int q) { return &fsx[fw][(q >> 2) & 1][A1 ? 0 : 4][0]; }
 };
 
 
@@ -134,22 +151,56 @@ __device__ __forceinline__ SegGeo seg_geo(const TvArgs& a, int vp) {
 
 // Position of a role's current row in the stream; advanced monotonically (the segment walk
 // runs only when a plane boundary is crossed).
+// The cursor also caches its segment's address geometry (plane / observation / mask bases, chain, noise
+// element base, GEN: the wave window's first column), recomputed only when the cursor enters a new segment:
+// the per-row address and noise-counter arithmetic of the front and back roles is then adds and one
+// multiply, with no integer division on their per-step paths.
+struct RowGeo {
+    size_t pbase;       // element offset of the (real) plane in the (B, C, H, ldw) state buffers
+    size_t ybase;       // element offset of the plane in the observation (chain stride y_cs)
+    size_t mbase;       // byte offset of the chain's mask (chain stride m_cs)
+    size_t ebase;       // unpadded element index of the plane's first element in its chain (noise counter)
+    int bb;             // chain (batch entry)
+    int f0;             // first column of the wave window (GEN; 0 otherwise)
+    int cc0, cc1;       // core columns of the segment
+};
 struct RowCursor {
     int q, s, p, r, qend;
+    RowGeo g;
 };
-__device__ __forceinline__ void cursor_seek(const RowMap& m, RowCursor& c) {
+template <bool GEN>
+__device__ __forceinline__ RowGeo row_geo(const TvArgs& a, int vp) {
+    const SegGeo sg = seg_geo<GEN>(a, vp);
+    const size_t HW = (size_t)a.H * a.ldw;
+    RowGeo g;
+    g.bb = sg.rp / a.C;
+    const int cc = sg.rp - g.bb * a.C;
+    g.pbase = (size_t)sg.rp * HW;
+    g.ybase = (size_t)g.bb * a.y_cs + (size_t)cc * HW;
+    g.mbase = (size_t)g.bb * a.m_cs;
+    g.ebase = (size_t)cc * a.H * a.W;
+    g.f0 = sg.f0;
+    g.cc0 = sg.cc0;
+    g.cc1 = sg.cc1;
+    return g;
+}
+template <bool GEN>
+__device__ __forceinline__ void cursor_seek(const TvArgs& a, const RowMap& m, RowCursor& c) {
     while (c.s + 1 < m.ns && c.q >= m.qs(c.s + 1)) ++c.s;
     c.qend = m.qs(c.s + 1);
     c.p = m.pl(c.s);
     c.r = m.lo(c.s) + (c.q - m.qs(c.s));
+    c.g = row_geo<GEN>(a, c.p);
 }
-__device__ __forceinline__ void cursor_init(const RowMap& m, RowCursor& c, int q) {
+template <bool GEN>
+__device__ __forceinline__ void cursor_init(const TvArgs& a, const RowMap& m, RowCursor& c, int q) {
     c.q = q; c.s = 0;
-    cursor_seek(m, c);
+    cursor_seek<GEN>(a, m, c);
 }
-__device__ __forceinline__ void cursor_advance(const RowMap& m, RowCursor& c, int d) {
+template <bool GEN>
+__device__ __forceinline__ void cursor_advance(const TvArgs& a, const RowMap& m, RowCursor& c, int d) {
     c.q += d; c.r += d;
-    if (c.q >= c.qend && c.s + 1 < m.ns) cursor_seek(m, c);
+    if (c.q >= c.qend && c.s + 1 < m.ns) cursor_seek<GEN>(a, m, c);
 }
 // stream index of the first segment start after stream row q (SP_NOSEG if none)
 __device__ __forceinline__ int next_seg_start(const RowMap& m, int q) {
@@ -265,8 +316,11 @@ __device__ __forceinline__ void stage_phase_b(const TvArgs& a, const StageRow& r
 // Segment edges (split mode): the first row of a segment has no row above (its primal
 // uses u0 = 0 above) and the last has no row below (its dual has no vertical difference);
 // the rel-err partial sums are flushed per segment (different segments may be different chains).
-template <bool EXACT, bool TRK, bool GEN>
-__device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, const RowMap& rm, int k, int n,
+// FIRST (A1 only): stage 1, which reads its input row straight from the front's DMA staging (the row's front
+// wave j % 4, slot (j / 4) % 3) instead of a ring -- a separate instantiation, so no stage branches on k around
+// its LDS reads.
+template <bool EXACT, bool TRK, bool GEN, bool A1, bool FIRST>
+__device__ __forceinline__ void stage_loop(const TvArgs& a, StreamSharedT<A1>& sh, const RowMap& rm, int k, int n,
                                            int nsteps, int Qk, int lane, int lastk, int nreal, bool core) {
     // GEN: the lane's columns change with the column segment of the row (row split over virtual
     // planes): lastk / nreal / core follow the primal row's segment; each row carries its lastk
@@ -307,18 +361,28 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
     };
     int t = 0;
     for (; t < tbeg; ++t) step_barrier();
+    const int rin = StreamSharedT<A1>::rk(k - 1), rout = StreamSharedT<A1>::rk(k);
     auto load_row = [&](int j, float4& X2, float4& U0, float4& U1, float4& YY) {
-        const int sl = j & 1;
-        X2 = sh.x2[k - 1][sl][lane];
-        U0 = sh.u0[k - 1][sl][lane];
-        U1 = sh.u1[k - 1][sl][lane];
+        float4 A, B;
+        if (FIRST) {
+            X2 = sh.stX(j & 3, j)[lane];
+            A = sh.stUa(j & 3, j)[lane];
+            B = sh.stUb(j & 3, j)[lane];
+        } else {
+            const int sl = j & 1;
+            X2 = sh.x2[rin][sl][lane];
+            A = sh.ua[rin][sl][lane];
+            B = sh.ub[rin][sl][lane];
+        }
         YY = sh.y[j & (SP_YRING - 1)][lane];
+        U0 = make_float4(A.x, A.z, B.x, B.z);
+        U1 = make_float4(A.y, A.w, B.y, B.w);
     };
     auto store_row = [&](int i, const StageRow& r, const float (&un0)[CPL], const float (&un1)[CPL]) {
         const int so = i & 1;
-        sh.x2[k][so][lane] = make_float4(r.x2n[0], r.x2n[1], r.x2n[2], r.x2n[3]);
-        sh.u0[k][so][lane] = make_float4(un0[0], un0[1], un0[2], un0[3]);
-        sh.u1[k][so][lane] = make_float4(un1[0], un1[1], un1[2], un1[3]);
+        sh.x2[rout][so][lane] = make_float4(r.x2n[0], r.x2n[1], r.x2n[2], r.x2n[3]);
+        sh.ua[rout][so][lane] = make_float4(un0[0], un1[0], un0[1], un1[1]);
+        sh.ub[rout][so][lane] = make_float4(un0[2], un1[2], un0[3], un1[3]);
     };
     // rows 0 and 1: primal update only (segments hold >= 2 rows: row 1 never starts one)
     {
@@ -392,7 +456,7 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamShared& sh, co
 // GEN: the row pitch is not the image width (rows padded: W % 4 != 0) -- the last-column, norm
 // and noise-window handling of such rows, compiled only into the kernels that need it
 template <bool EXACT, bool ALPHA1, bool GEN>
-__device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, const RowMap& rm, const int n,
+__device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA1>& sh, const RowMap& rm, const int n,
                                             const bool track, const long long step, const bool fresh) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (scalar branches)
@@ -403,7 +467,6 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
     const size_t BE = (size_t)a.B * E;
     const int par_in = (int)(step & 1), par_out = (int)((step + 1) & 1);
     const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    auto plane_off = [&](int pl) -> size_t { return (size_t)pl * HW; };   // planes are (b, c) in NCHW order
     const int Q = rm.Q;
     const int qc0 = rm.htop, qc1 = Q - rm.hbot;          // core stream rows
     // column geometry of the first row's segment (the only one without GEN)
@@ -444,121 +507,133 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         // per front wave), row and column clamped into the plane so every lane loads.
         const int gjc = min(gj0, L - CPL);
         RowCursor rc_cur, rc_dma;
-        cursor_init(rm, rc_cur, min(fw, Q - 1));
-        cursor_init(rm, rc_dma, min(fw, Q - 1));
+        cursor_init<GEN>(a, rm, rc_cur, min(fw, Q - 1));
+        cursor_init<GEN>(a, rm, rc_dma, min(fw, Q - 1));
         // part `part` of the loads of stream row q: 0 = X, 1 = y, 2 = u2 (two halves), 3 = mask (+ x2)
         auto front_issue = [&](int part, int q, const RowCursor& rc) {
             const int rr = min(rc.r, H - 1);
             const int bi = (q >> 2) & 1;
-            const SegGeo g = seg_geo<GEN>(a, rc.p);
-            const int gjr = GEN ? min(g.f0 + CPL * lane, L - CPL) : gjc;
-            const int bb = g.rp / C;
+            const int gjr = GEN ? min(rc.g.f0 + CPL * lane, L - CPL) : gjc;
             // 64-bit per-lane addresses (the SGPR-base form measured +12 % in round 2:
             // this kernel's row cursor sits in VGPRs, so each DMA pays two readfirstlane + 5 wait states)
-            const size_t base = plane_off(g.rp) + (size_t)rr * L + gjr;
+            const size_t roff = (size_t)rr * L + gjr;
+            const size_t base = rc.g.pbase + roff;
             if (part == 0) {
-                glds16(xin + base, &sh.fst[fw][bi][0][0]);
+                glds16(xin + base, sh.stX(fw, q));
             } else if (part == 1) {
-                glds16(a.yobs + (size_t)bb * a.y_cs + (size_t)(g.rp - bb * C) * HW + (size_t)rr * L + gjr,
-                       &sh.fst[fw][bi][1][0]);
+                glds16(a.yobs + rc.g.ybase + roff, sh.stY(fw, q));
             } else if (part == 2) {
-                glds16(u2in + 2 * base, &sh.fst[fw][bi][2][0]);
-                glds16(u2in + 2 * base + 4, &sh.fst[fw][bi][3][0]);
+                glds16(u2in + 2 * base, sh.stUa(fw, q));
+                glds16(u2in + 2 * base + 4, sh.stUb(fw, q));
             } else {
-                if (!ALPHA1) glds16(x2in + base, &sh.fst[fw][bi][4][0]);
-                glds4(a.mask + (size_t)bb * a.m_cs + (size_t)rr * L + gjr, &sh.fmk[fw][bi][0]);
+                if (!ALPHA1) glds16(x2in + base, sh.stX2(fw, q));
+                glds4(a.mask + rc.g.mbase + roff, &sh.fmk[fw][bi][0]);
             }
         };
         // row fw's loads up front; afterwards the loads of row q + 4 are issued one part per
         // phase of row q (into the buffer of row q - 4, consumed before phase 0 of row q), so
         // their issue cost is spread over four steps
         for (int part = 0; part < 4; ++part) front_issue(part, fw, rc_dma);
-        cursor_advance(rm, rc_dma, min(4, max(0, Q - 1 - fw)));
-        for (int t = 0; t < nsteps; ++t) {
-                // ======================= FRONT =======================
-                const int p = (t + 4 - fw) & 3;
-                const int q = t - p;
-                if (q >= 0 && q < Q) {
-                    if (p < 3) front_issue(p, q + 4, rc_dma);
-                    if (p == 0) {
-                        const SegGeo g = seg_geo<GEN>(a, rc_cur.p);
-                        const int bb = g.rp / C, cc = g.rp - bb * C;
-                        if (GEN) {                                  // this row's segment's lanes
-                            gjf = g.f0 + CPL * lane;
-                            okf = gjf < W;
-                        }
-                        // element index in the chain's unpadded C*H*W image: the noise stream
-                        // does not depend on the row pitch
-                        const size_t e = ((size_t)cc * H + rc_cur.r) * W + gjf;
-                        esh = (int)(e & 3);                         // the same for every lane of the row
-                        uint32_t c0 = (uint32_t)(e >> 2), c1 = (uint32_t)step, c2 = TAG_LANGEVIN,
-                                 c3 = (uint32_t)(a.seed >> 32);
-                        philox4x32_10(c0, c1, c2, c3, (uint32_t)a.seed, (uint32_t)(a.chain0 + bb));
-                        ph0 = c0; ph1 = c1; ph2 = c2; ph3 = c3;
-                        if (GEN && esh != 0) {                     // the lane's 4 elements span two quads
-                            uint32_t d0 = (uint32_t)(e >> 2) + 1u, d1 = (uint32_t)step, d2 = TAG_LANGEVIN,
-                                     d3 = (uint32_t)(a.seed >> 32);
-                            philox4x32_10(d0, d1, d2, d3, (uint32_t)a.seed, (uint32_t)(a.chain0 + bb));
-                            pq0 = d0; pq1 = d1; pq2 = d2; pq3 = d3;
-                        }
-                    } else if (p == 1) {
-                        box_muller(ph0, ph1, zn0, zn1);
-                        if (GEN && esh != 0) box_muller(pq0, pq1, zq0, zq1);
-                    } else if (p == 2) {
-                        box_muller(ph2, ph3, zn2, zn3);
-                        if (GEN && esh != 0) {
-                            box_muller(pq2, pq3, zq2, zq3);
-                            // element i of the lane = output (esh + i) of the two-quad window
-                            const float w8[8] = {zn0, zn1, zn2, zn3, zq0, zq1, zq2, zq3};
-                            float r4[CPL];
+        cursor_advance<GEN>(a, rm, rc_dma, min(4, max(0, Q - 1 - fw)));
+        // ======================= FRONT =======================
+        // Row q (q % 4 == fw) runs its four phases in steps q .. q + 3: the loop below is unrolled by
+        // phase (one step barrier after each), so no step decides its phase at run time.
+        int t = 0;
+        for (; t < fw && t < nsteps; ++t) step_barrier();
+        for (int q = fw; q < Q; q += 4) {
+            // ---- phase 0: Philox of row q; DMA part 0 of row q + 4
+            front_issue(0, q + 4, rc_dma);
+            {
+                const RowGeo& g = rc_cur.g;
+                if (GEN) {                                  // this row's segment's lanes
+                    gjf = g.f0 + CPL * lane;
+                    okf = gjf < W;
+                }
+                // element index in the chain's unpadded C*H*W image: the noise stream
+                // does not depend on the row pitch
+                const size_t e = g.ebase + (size_t)rc_cur.r * W + gjf;
+                esh = (int)(e & 3);                         // the same for every lane of the row
+                uint32_t c0 = (uint32_t)(e >> 2), c1 = (uint32_t)step, c2 = TAG_LANGEVIN,
+                         c3 = (uint32_t)(a.seed >> 32);
+                philox4x32_10(c0, c1, c2, c3, (uint32_t)a.seed, (uint32_t)(a.chain0 + g.bb));
+                ph0 = c0; ph1 = c1; ph2 = c2; ph3 = c3;
+                if (GEN && esh != 0) {                     // the lane's 4 elements span two quads
+                    uint32_t d0 = (uint32_t)(e >> 2) + 1u, d1 = (uint32_t)step, d2 = TAG_LANGEVIN,
+                             d3 = (uint32_t)(a.seed >> 32);
+                    philox4x32_10(d0, d1, d2, d3, (uint32_t)a.seed, (uint32_t)(a.chain0 + g.bb));
+                    pq0 = d0; pq1 = d1; pq2 = d2; pq3 = d3;
+                }
+            }
+            step_barrier();
+            // ---- phase 1: Box-Muller pair 1; DMA part 1
+            front_issue(1, q + 4, rc_dma);
+            box_muller(ph0, ph1, zn0, zn1);
+            if (GEN && esh != 0) box_muller(pq0, pq1, zq0, zq1);
+            step_barrier();
+            // ---- phase 2: Box-Muller pair 2; DMA part 2
+            front_issue(2, q + 4, rc_dma);
+            box_muller(ph2, ph3, zn2, zn3);
+            if (GEN && esh != 0) {
+                box_muller(pq2, pq3, zq2, zq3);
+                // element i of the lane = output (esh + i) of the two-quad window
+                const float w8[8] = {zn0, zn1, zn2, zn3, zq0, zq1, zq2, zq3};
+                float r4[CPL];
 #pragma unroll
-                            for (int i = 0; i < CPL; ++i)
-                                r4[i] = esh == 1 ? w8[i + 1] : (esh == 2 ? w8[i + 2] : w8[i + 3]);
-                            zn0 = r4[0]; zn1 = r4[1]; zn2 = r4[2]; zn3 = r4[3];
-                        }
+                for (int i = 0; i < CPL; ++i)
+                    r4[i] = esh == 1 ? w8[i + 1] : (esh == 2 ? w8[i + 2] : w8[i + 3]);
+                zn0 = r4[0]; zn1 = r4[1]; zn2 = r4[2]; zn3 = r4[3];
+            }
+            step_barrier();
+            // ---- phase 3: data term of row q -> ring 0 / Y ring; DMA part 3 of row q + 4
+            {
+                wait_vm<4>();   // row q's loads landed; parts 0-2 of row q + 4 may fly
+                const int bi = (q >> 2) & 1;
+                const float4 fX = sh.stX(fw, q)[lane];
+                const float4 fYo = sh.stY(fw, q)[lane];
+                const uint32_t fMw = sh.fmk[fw][bi][lane];
+                const float X[CPL] = {fX.x, fX.y, fX.z, fX.w};
+                const float yo[CPL] = {fYo.x, fYo.y, fYo.z, fYo.w};
+                const float mk[CPL] = {(float)(fMw & 0xFFu), (float)((fMw >> 8) & 0xFFu),
+                                       (float)((fMw >> 16) & 0xFFu), (float)(fMw >> 24)};
+                const float Z[CPL] = {zn0, zn1, zn2, zn3};
+                float Yv[CPL];
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    if (EXACT) {
+                        const float g = (-mk[k] * (X[k] - yo[k])) / a.sigma2;
+                        Yv[k] = okf ? (X[k] + a.c1 * g) + a.c2 * Z[k] : 0.f;
                     } else {
-                        wait_vm<ALPHA1 ? 4 : 4>();   // row q's loads landed; parts 0-2 of row q + 4 may fly
-                        const int bi = (q >> 2) & 1;
-                        const float4 fX = sh.fst[fw][bi][0][lane];
-                        const float4 fYo = sh.fst[fw][bi][1][lane];
-                        const float4 fU0 = sh.fst[fw][bi][2][lane];
-                        const float4 fU1 = sh.fst[fw][bi][3][lane];
-                        const float4 fXS = ALPHA1 ? zero4 : sh.fst[fw][bi][4][lane];
-                        const uint32_t fMw = sh.fmk[fw][bi][lane];
-                        const float X[CPL] = {fX.x, fX.y, fX.z, fX.w};
-                        const float yo[CPL] = {fYo.x, fYo.y, fYo.z, fYo.w};
-                        const float mk[CPL] = {(float)(fMw & 0xFFu), (float)((fMw >> 8) & 0xFFu),
-                                               (float)((fMw >> 16) & 0xFFu), (float)(fMw >> 24)};
-                        const float Z[CPL] = {zn0, zn1, zn2, zn3};
-                        float Yv[CPL];
-#pragma unroll
-                        for (int k = 0; k < CPL; ++k) {
-                            if (EXACT) {
-                                const float g = (-mk[k] * (X[k] - yo[k])) / a.sigma2;
-                                Yv[k] = okf ? (X[k] + a.c1 * g) + a.c2 * Z[k] : 0.f;
-                            } else {
-                                const float g = (mk[k] * (yo[k] - X[k])) * a.inv_sigma2;
-                                Yv[k] = okf ? __builtin_fmaf(a.c2, Z[k], __builtin_fmaf(a.c1, g, X[k])) : 0.f;
-                            }
-                        }
-                        const float4 Y4 = make_float4(Yv[0], Yv[1], Yv[2], Yv[3]);
-                        float4 x2s;
-                        if (fresh) x2s = Y4;
-                        else x2s = ALPHA1 ? fX : fXS;
-                        if (!okf) x2s = zero4;
-                        const int s0 = q & 1;
-                        sh.x2[0][s0][lane] = x2s;
-                        sh.u0[0][s0][lane] = fresh ? zero4 : make_float4(fU0.x, fU0.z, fU1.x, fU1.z);
-                        sh.u1[0][s0][lane] = fresh ? zero4 : make_float4(fU0.y, fU0.w, fU1.y, fU1.w);
-                        sh.y[q & (SP_YRING - 1)][lane] = Y4;
-                            // the wave's next rows: noise row q + 4, DMA of row q + 8... issued as q + 4
-                        front_issue(3, q + 4, rc_dma);
-                        cursor_advance(rm, rc_cur, 4);
-                        if (q + 8 < Q) cursor_advance(rm, rc_dma, 4);
+                        const float g = (mk[k] * (yo[k] - X[k])) * a.inv_sigma2;
+                        Yv[k] = okf ? __builtin_fmaf(a.c2, Z[k], __builtin_fmaf(a.c1, g, X[k])) : 0.f;
                     }
                 }
+                const float4 Y4 = make_float4(Yv[0], Yv[1], Yv[2], Yv[3]);
+                if (ALPHA1) {
+                    // stage 1 reads x2 = X and u2 from this staging; a TV restart (fresh) makes them Y and 0
+                    // (lanes beyond the image keep the DMA'd values: they never feed an image column)
+                    if (fresh) {
+                        sh.stX(fw, q)[lane] = okf ? Y4 : zero4;
+                        sh.stUa(fw, q)[lane] = zero4;
+                        sh.stUb(fw, q)[lane] = zero4;
+                    }
+                } else {
+                    float4 x2s = fresh ? Y4 : sh.stX2(fw, q)[lane];
+                    if (!okf) x2s = zero4;
+                    const int s0 = q & 1;
+                    sh.x2[0][s0][lane] = x2s;
+                    sh.ua[0][s0][lane] = fresh ? zero4 : sh.stUa(fw, q)[lane];
+                    sh.ub[0][s0][lane] = fresh ? zero4 : sh.stUb(fw, q)[lane];
+                }
+                sh.y[q & (SP_YRING - 1)][lane] = Y4;
+                // the wave's next rows: noise row q + 4, DMA of row q + 8... issued as q + 4
+                front_issue(3, q + 4, rc_dma);
+                cursor_advance<GEN>(a, rm, rc_cur, 4);
+                if (q + 8 < Q) cursor_advance<GEN>(a, rm, rc_dma, 4);
+            }
             step_barrier();
+            t += 4;
         }
+        for (; t < nsteps; ++t) step_barrier();
     } else if (role == 1) {
         // ---------------- STAGE (one inner TV iteration per wave) ----------------
         // the only column whose forward difference is forced to 0 is the image's right edge;
@@ -568,8 +643,9 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         const int nreal = min(CPL, max(0, W - gj0));      // real (non-pitch-padding) columns of the lane
         __builtin_amdgcn_s_setprio(1);
         const int qk = stage_rows(k_st);
-        if (trk) stage_loop<EXACT, true, GEN>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core);
-        else stage_loop<EXACT, false, GEN>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core);
+        if (ALPHA1 && k_st == 1) stage_loop<EXACT, false, GEN, ALPHA1, true>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core);
+        else if (trk) stage_loop<EXACT, true, GEN, ALPHA1, false>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core);
+        else stage_loop<EXACT, false, GEN, ALPHA1, false>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core);
     } else if (role == 3) {
         for (int t = 0; t < nsteps; ++t) step_barrier();
     } else {
@@ -585,15 +661,14 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         const bool need_prev = si.acc && !si.first;
         const int gjc = min(gj0, L - CPL);
         RowCursor rc_cur, rc_dma;
-        cursor_init(rm, rc_cur, min(bw, Q - 1));
-        cursor_init(rm, rc_dma, min(bw, Q - 1));
+        cursor_init<GEN>(a, rm, rc_cur, min(bw, Q - 1));
+        cursor_init<GEN>(a, rm, rc_dma, min(bw, Q - 1));
         auto back_issue = [&](int q, const RowCursor& rc) {
             if (need_prev) {
                 const int rr = min(rc.r, H - 1);
                 const int bi = (q >> 1) & 1;
-                const SegGeo g = seg_geo<GEN>(a, rc.p);
-                const int gjr = GEN ? min(g.f0 + CPL * lane, L - CPL) : gjc;
-                const size_t base = plane_off(g.rp) + (size_t)rr * L + gjr;
+                const int gjr = GEN ? min(rc.g.f0 + CPL * lane, L - CPL) : gjc;
+                const size_t base = rc.g.pbase + (size_t)rr * L + gjr;
                 glds16(mean_in + base, &sh.bst[bw][bi][0][0]);
                 glds16(sq_in + base, &sh.bst[bw][bi][1][0]);
             }
@@ -603,7 +678,6 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         // a row's stores are spread over the wave's two steps: state + accumulators, then the rest
         bool hold = false, hcore = core;
         size_t h_base = 0;                  // per-lane element index
-        uint32_t h_vo = 0;                  // the lane's column as a byte offset
         float4 hM = zero4, hQ = zero4, hX = zero4;
         auto flush_held = [&]() {
             if (!(GEN ? hcore : core)) return;
@@ -621,88 +695,100 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
         // mean / sq rows are LDS-DMA'd two of the wave's rows ahead (4 stream rows); c1 / c2 =
         // vector-memory ops issued after the DMA of the wave's next / next-but-one row
         back_issue(bw, rc_dma);
-        if (bw + 2 < Q) cursor_advance(rm, rc_dma, 2);
+        if (bw + 2 < Q) cursor_advance<GEN>(a, rm, rc_dma, 2);
         back_issue(bw + 2, rc_dma);
         int c1 = 2, c2 = 0;
-        for (int t = 0; t < nsteps; ++t) {
-                // ======================= BACK =======================
-                const int q = t - 4 - 3 * n;
-                if (q >= 0 && q < Qb && (q & 1) == bw) {
-                    const int sl = q & 1;
-                    // stage n wrote ring n row q at step t - 1
-                    const float4 X2 = sh.x2[n][sl][lane];
-                    const float4 U0 = sh.u0[n][sl][lane];
-                    const float4 U1 = sh.u1[n][sl][lane];
-                    float4 Xo = X2;
-                    if (!ALPHA1) {
-                        const float4 YY = sh.y[q & (SP_YRING - 1)][lane];
-                        Xo.x = (1.0f - a.alpha) * YY.x + a.alpha * X2.x;
-                        Xo.y = (1.0f - a.alpha) * YY.y + a.alpha * X2.y;
-                        Xo.z = (1.0f - a.alpha) * YY.z + a.alpha * X2.z;
-                        Xo.w = (1.0f - a.alpha) * YY.w + a.alpha * X2.w;
+        // ======================= BACK =======================
+        // Row q (q % 2 == bw) leaves the pipeline at step q + 4 + 3n (stage n wrote ring n row q in the step
+        // before); its accumulator / sample stores go out in the wave's next step.  Unrolled by those two
+        // steps (a step barrier after each), so no step decides at run time whether it has a row.
+        int t = 0;
+        const int t0 = 4 + 3 * n + bw;
+        for (; t < t0 && t < nsteps; ++t) step_barrier();
+        for (int q = bw; q < Qb && t < nsteps; q += 2) {
+            {
+                const int sl = q & 1;
+                // stage n wrote ring n row q at step t - 1
+                const int rn = StreamSharedT<ALPHA1>::rk(n);
+                const float4 X2 = sh.x2[rn][sl][lane];
+                const float4 UA = sh.ua[rn][sl][lane];
+                const float4 UB = sh.ub[rn][sl][lane];
+                float4 Xo = X2;
+                if (!ALPHA1) {
+                    const float4 YY = sh.y[q & (SP_YRING - 1)][lane];
+                    Xo.x = (1.0f - a.alpha) * YY.x + a.alpha * X2.x;
+                    Xo.y = (1.0f - a.alpha) * YY.y + a.alpha * X2.y;
+                    Xo.z = (1.0f - a.alpha) * YY.z + a.alpha * X2.z;
+                    Xo.w = (1.0f - a.alpha) * YY.w + a.alpha * X2.w;
+                }
+                float4 M4 = zero4, Q4 = zero4;
+                if (si.acc) {
+                    float4 bm = zero4, bq = zero4;
+                    if (need_prev) {
+                        // DMA of row q was issued just before the previous row's stores
+                        wait_vm_n(c1);
+                        bm = sh.bst[bw][(q >> 1) & 1][0][lane];
+                        bq = sh.bst[bw][(q >> 1) & 1][1][lane];
                     }
-                    float4 M4 = zero4, Q4 = zero4;
-                    if (si.acc) {
-                        float4 bm = zero4, bq = zero4;
-                        if (need_prev) {
-                            // DMA of row q was issued just before the previous row's stores
-                            wait_vm_n(c1);
-                            bm = sh.bst[bw][(q >> 1) & 1][0][lane];
-                            bq = sh.bst[bw][(q >> 1) & 1][1][lane];
-                        }
-                        const float xs[CPL] = {Xo.x, Xo.y, Xo.z, Xo.w};
-                        const float ms[CPL] = {bm.x, bm.y, bm.z, bm.w};
-                        const float qs[CPL] = {bq.x, bq.y, bq.z, bq.w};
-                        float m[CPL], qq[CPL];
+                    const float xs[CPL] = {Xo.x, Xo.y, Xo.z, Xo.w};
+                    const float ms[CPL] = {bm.x, bm.y, bm.z, bm.w};
+                    const float qs[CPL] = {bq.x, bq.y, bq.z, bq.w};
+                    float m[CPL], qq[CPL];
 #pragma unroll
-                        for (int kk = 0; kk < CPL; ++kk) {
-                            if (si.first) {
-                                m[kk] = si.cb * xs[kk];
-                                qq[kk] = si.cb * (xs[kk] * xs[kk]);
-                            } else {
-                                m[kk] = si.ca * ms[kk] + si.cb * xs[kk];
-                                qq[kk] = si.ca * qs[kk] + si.cb * (xs[kk] * xs[kk]);
-                            }
+                    for (int kk = 0; kk < CPL; ++kk) {
+                        if (si.first) {
+                            m[kk] = si.cb * xs[kk];
+                            qq[kk] = si.cb * (xs[kk] * xs[kk]);
+                        } else {
+                            m[kk] = si.ca * ms[kk] + si.cb * xs[kk];
+                            qq[kk] = si.ca * qs[kk] + si.cb * (xs[kk] * xs[kk]);
                         }
-                        M4 = make_float4(m[0], m[1], m[2], m[3]);
-                        Q4 = make_float4(qq[0], qq[1], qq[2], qq[3]);
                     }
-                    // all LDS reads of this row (ring + staging) done before the staging
-                    // buffer is re-targeted by the next DMA
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    const RowCursor rc = rc_cur;
-                    cursor_advance(rm, rc_cur, 2);
-                    if (q + 4 < Q) cursor_advance(rm, rc_dma, 2);
-                    back_issue(q + 4, rc_dma);   // into the buffer just consumed (rows q, q + 4 share it)
-                    asm volatile("" ::: "memory");
-                    const bool rowcore = q >= qc0 && q < qc1;
-                    {
-                        const int ns = rowcore ? nst : 0;   // this row's stores (both steps)
-                        c1 = c2 + 2 + ns;
-                        c2 = ns;
-                    }
-                    // GEN: the lanes' columns of this row's segment
-                    const SegGeo gr = seg_geo<GEN>(a, rc.p);
-                    const int gjr = GEN ? gr.f0 + CPL * lane : gj0;
-                    const bool corer = GEN ? (gjr < W && gjr >= gr.cc0 && gjr < gr.cc1) : core;
-                    if (rowcore && corer) {
-                        const size_t base = plane_off(gr.rp) + (size_t)rc.r * L + gjr;
-                        st_nt(a.x[par_out] + base, Xo);
-                        float* u2o = a.u2[par_out] + 2 * base;
-                        st_nt(u2o, make_float4(U0.x, U1.x, U0.y, U1.y));
-                        st_nt(u2o + 4, make_float4(U0.z, U1.z, U0.w, U1.w));
-                        if (!ALPHA1) st_nt(a.x2[par_out] + base, X2);
-                        // the accumulator / sample stores go out in the wave's next (idle) step
-                        h_base = base; hM = M4; hQ = Q4; hX = Xo;
-                    }
-                    hold = rowcore;
-                    if (GEN) hcore = corer;
-                } else if (hold) {
+                    M4 = make_float4(m[0], m[1], m[2], m[3]);
+                    Q4 = make_float4(qq[0], qq[1], qq[2], qq[3]);
+                }
+                // all LDS reads of this row (ring + staging) done before the staging
+                // buffer is re-targeted by the next DMA
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const RowCursor rc = rc_cur;
+                cursor_advance<GEN>(a, rm, rc_cur, 2);
+                if (q + 4 < Q) cursor_advance<GEN>(a, rm, rc_dma, 2);
+                back_issue(q + 4, rc_dma);   // into the buffer just consumed (rows q, q + 4 share it)
+                asm volatile("" ::: "memory");
+                const bool rowcore = q >= qc0 && q < qc1;
+                {
+                    const int ns = rowcore ? nst : 0;   // this row's stores (both steps)
+                    c1 = c2 + 2 + ns;
+                    c2 = ns;
+                }
+                // GEN: the lanes' columns of this row's segment
+                const int gjr = GEN ? rc.g.f0 + CPL * lane : gj0;
+                const bool corer = GEN ? (gjr < W && gjr >= rc.g.cc0 && gjr < rc.g.cc1) : core;
+                if (rowcore && corer) {
+                    const size_t base = rc.g.pbase + (size_t)rc.r * L + gjr;
+                    st_nt(a.x[par_out] + base, Xo);
+                    float* u2o = a.u2[par_out] + 2 * base;
+                    st_nt(u2o, UA);
+                    st_nt(u2o + 4, UB);
+                    if (!ALPHA1) st_nt(a.x2[par_out] + base, X2);
+                    // the accumulator / sample stores go out in the wave's next (idle) step
+                    h_base = base; hM = M4; hQ = Q4; hX = Xo;
+                }
+                hold = rowcore;
+                if (GEN) hcore = corer;
+            }
+            step_barrier();
+            ++t;
+            if (t < nsteps) {
+                if (hold) {
                     flush_held();
                     hold = false;
                 }
-            step_barrier();
+                step_barrier();
+                ++t;
+            }
         }
+        for (; t < nsteps; ++t) step_barrier();
         if (hold) flush_held();
     }
 
@@ -712,7 +798,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamShared& sh, c
 
 template <bool EXACT, bool ALPHA1, bool GEN>
 __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
-    __shared__ StreamShared sh;
+    __shared__ StreamSharedT<ALPHA1> sh;
     __shared__ int s_stop[MAXG];
     __shared__ int s_flag, s_item, s_next;
     const int C = a.C;

@@ -1,8 +1,7 @@
 """Per-step barrier accounting of the row-stream kernel from the diagnostic library built by
 `python3 tools/variant_build.py sdiag tools/patches/stream_stepdiag.py` (exp_libs/lib_sdiag.so).
-Prints, averaged over workgroups 0..63 of one bench-shape launch: the step length, the latest arrival (the
-pole's work), the release latency after the last arrival, each wave's work, and how often each wave is the
-last to arrive.  Usage: PSGLA_LIB=exp_libs/lib_sdiag.so python3 tools/stream_stepdiag.py [B]"""
+Prints, averaged over workgroups 0..63 of one bench-shape launch: the step length, each wave's work (its
+arrival - its release), and how often each wave is the last to arrive.  Usage: PSGLA_LIB=exp_libs/lib_sdiag.so python3 tools/stream_stepdiag.py [B]"""
 import ctypes
 import os
 import sys
@@ -46,7 +45,7 @@ d = buf.cpu().numpy().astype(np.float64)
 n = d[:, 0]
 per = lambda col: (d[:, col] / n).mean()  # noqa: E731
 print(f"stream B={B}: launch {ms*1e3:.1f} us (diag build); steps per workgroup {n.mean():.1f}")
-print(f"  per step (s_memtime ticks): length {per(1):.0f}  latest arrival {per(3):.0f}  release after last arrival {per(2):.0f}")
+print(f"  per step (s_memtime ticks): length {per(1):.0f}")
 roles = ["front"] * 4 + [f"stage{k}" for k in range(1, 11)] + ["back"] * 2
 for w in range(16):
     print(f"  w{w:2d} {roles[w]:>7s}: work {per(4 + w):6.0f}   last to arrive in {100 * (d[:, 20 + w] / n).mean():5.1f} % of steps")

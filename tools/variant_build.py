@@ -4,7 +4,10 @@ searched over every translation unit (and psgla_common.hpp); the build fails if 
 differs.  Only the units whose text changed are recompiled -- the others reuse the product objects in
 build/obj (run ``python -m psgla_for_posterior_sampling_amd.build`` first); a changed header recompiles all.
 Usage: python3 tools/variant_build.py NAME PATCHES.py [NAME2 PATCHES2.py ...]
-       (PATCHES.py defines PATCHES = [(old, new, count), ...]; extra hipcc flags: EXTRA = ["-D...", ...])"""
+       (PATCHES.py defines PATCHES = [(old, new, count), ...]; extra hipcc flags: EXTRA = ["-D...", ...];
+        FORCE = ["tv_stream.hip", ...] recompiles those units from the working tree even if no patch touches them;
+        SOURCE_OVERRIDE = {"tv_stream.hip": "/path/file.hip"} takes a unit's text from another file, e.g. a
+        committed version, before the patches apply)"""
 import os
 import runpy
 import shutil
@@ -19,6 +22,8 @@ def variant(name, patch_file):
     spec = runpy.run_path(patch_file)
     files = {os.path.basename(p): open(p).read() for p in B.SOURCES + [os.path.join(B.CSRC, "psgla_common.hpp")]}
     orig = dict(files)
+    for unit, path in spec.get("SOURCE_OVERRIDE", {}).items():   # e.g. a unit as committed (git show) as the base
+        files[unit] = open(path).read()
     for old, new, count in spec.get("PATCHES", []):
         total = sum(t.count(old) for t in files.values())
         if total != count:
@@ -33,7 +38,7 @@ def variant(name, patch_file):
         open(os.path.join(src_dir, k), "w").write(t)
     shutil.copy(os.path.join(B.CSRC, "noise.hpp"), src_dir)
     extra = list(spec.get("EXTRA", []))
-    changed = [k for k in files if files[k] != orig[k]]
+    changed = [k for k in files if files[k] != orig[k]] + list(spec.get("FORCE", []))
     rebuild_all = "psgla_common.hpp" in changed or extra
     units = [os.path.join(src_dir, os.path.basename(s)) for s in B.SOURCES
              if rebuild_all or os.path.basename(s) in changed]
