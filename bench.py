@@ -72,6 +72,9 @@ def parse():
     p.add_argument("--kernel-iters", type=int, default=50)
     p.add_argument("--tv-iters", type=int, default=10, help="TV n_it_max (analysis only; the workload is 10)")
     p.add_argument("--stream-wgs", type=int, default=0, help="stream kernel work split (0 auto, -1 per plane)")
+    p.add_argument("--stream-windows", choices=["auto", "whole", "half"], default="auto",
+                   help="stream kernel column windows (auto: half-wave windows where they idle fewer lanes; "
+                        "half: always, a diagnostic)")
     p.add_argument("--variant", choices=["auto", "band", "stream", "tile"], default="auto",
                    help="fused TV kernel (analysis; auto = the library's choice)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the batch-1 CPU leg")
@@ -236,7 +239,7 @@ def main():
                         sigma2=float(np.float32(sigma1 ** 2)), alpha=1.0, ths=float(np.float32(s)),
                         tv=K.TvConstants(n_it_max=args.tv_iters), seed=0, n_iter=n_iter + args.kernel_iters,
                         n_inter=n_inter, n_inter_mmse=nm, chain0=c0, exact=args.exact,
-                        stream_wgs=args.stream_wgs, kernel_variant=args.variant)
+                        stream_wgs=args.stream_wgs, kernel_variant=args.variant, stream_windows=args.stream_windows)
     # warm-up: eager steps + graph capture + one replay
     eng.step(w_eager)
     eng.capture(gs)

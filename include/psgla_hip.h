@@ -133,6 +133,11 @@ typedef struct PsglaTvStep {
                                  copies [K][B][n_tv][2] and the tile kernel spreads its workgroups'
                                  rel-err partial sums over them (workgroup x adds to copy x % K), so
                                  that many tiles of one chain do not queue on the same atomics   */
+    int32_t stream_windows;   /* (ABI 9) row-stream column windows: 0 auto (256 < W <= 324 at n_tv = 10:
+                                 half-wave windows, two 128-column segments per wave, where whole
+                                 256-column windows would leave a third of the lanes idle); 1 whole
+                                 256-column windows only; 2 half-wave windows whenever they fit
+                                 (diagnostic: the halo cost of 128-column pipelines at any width)  */
 } PsglaTvStep;
 
 int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream);

@@ -95,24 +95,27 @@ static int tile_geometry(int P, int H, int nsegs, int h, int NW, int R, int* ban
     return ((P * nb * nsegs + 7) / 8) * 8;
 }
 
-// Column segments of the streaming kernel: equal core widths (multiples of 4) cut from the image
-// width W; segment s's wave covers columns [f0, f0 + 256) with f0 = (cc0 - h) & ~3 (cc0 = s * seg_w),
-// which must reach cc1 + h for interior cuts (the TV dependency cone) and the row pitch L at the
-// image's right end (no halo needed at the image edges).  Fewest segments; 0 if none fits.
-static int stream_segments(int W, int L, int h, int* seg_w) {
+// Column segments of the streaming kernel: core widths seg_w (a multiple of 4; the last segment takes the rest)
+// cut from the image width W; segment s's window of `win` columns starts at f0 = (cc0 - h) & ~3 (cc0 = s * seg_w)
+// and must reach cc1 + h for interior cuts (the TV dependency cone) and the row pitch L at the image's right end
+// (no halo needed at the image edges).  Fewest segments (then the widest seg_w from ceil(W / n) down); 0 if none
+// fits.  win = 256: a wave's window (4 columns x 64 lanes); 128: a half-wave's (st_half).
+static int stream_segments(int W, int L, int h, int* seg_w, int win = TV_COLS) {
     for (int n = 1; n <= 64; ++n) {
-        const int sw = (((W + n - 1) / n) + 3) & ~3;
-        if ((long long)sw * (n - 1) >= W) continue;         // last segment would be empty
-        bool ok = true;
-        for (int sgi = 0; sgi < n && ok; ++sgi) {
-            const int cc0 = sgi * sw, cc1 = min(W, cc0 + sw);
-            const int f0 = max(0, cc0 - h) & ~3;
-            const int need = (cc1 >= W) ? L : min(L, cc1 + h);
-            ok = need - f0 <= TV_COLS;
-        }
-        if (ok) {
-            if (seg_w) *seg_w = sw;
-            return n;
+        const int sw0 = (((W + n - 1) / n) + 3) & ~3;
+        for (int sw = sw0; sw >= 4 && sw >= sw0 - 32; sw -= 4) {
+            if ((long long)sw * (n - 1) >= W) continue;         // last segment would be empty
+            bool ok = true;
+            for (int sgi = 0; sgi < n && ok; ++sgi) {
+                const int cc0 = sgi * sw, cc1 = (sgi == n - 1) ? W : min(W, cc0 + sw);
+                const int f0 = max(0, cc0 - h) & ~3;
+                const int need = (cc1 >= W) ? L : min(L, cc1 + h);
+                ok = need - f0 <= win;
+            }
+            if (ok) {
+                if (seg_w) *seg_w = sw;
+                return n;
+            }
         }
     }
     return 0;
@@ -140,9 +143,9 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
         if (FRONT == FRONT_INPAINT && a.stream) {
             TvArgs s = a;
             s.fin_inline = (mask & 2) ? 1 : 0;
-            const int grid = s.split_wgs > 0 ? s.split_wgs : P * s.st_nsegs;   // virtual planes
+            const int grid = s.split_wgs > 0 ? s.split_wgs : s.st_nvp;   // virtual planes
             const bool gen = !(s.ldw == s.W && s.st_nsegs == 1);
-            launch_stream(s, dim3(grid), st, EXACT, ALPHA1, gen);
+            launch_stream(s, dim3(grid), st, EXACT, ALPHA1, gen, s.st_half != 0);
             int rc = launch_check("tv_stream_kernel");
             if (rc) return rc;
             return 0;                    // finalised in-kernel (or main pass only)
@@ -244,7 +247,20 @@ static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
     if (a.stream) {
         a.st_halo = d->n_tv;
         a.st_nsegs = stream_segments(a.W, a.ldw, d->n_tv, &a.st_seg_w);
-        if (choose_split((long long)d->B * d->C * a.st_nsegs, d->H, d->n_tv, d->stream_wgs, &a.split_wgs)) {
+        a.st_half = 0;
+        a.st_nvp = d->B * d->C * a.st_nsegs;
+        // half windows when they leave fewer lanes idle (castle-like 481 x 321: 2 windows of 256 columns hold
+        // 321 -- 63 % of the lanes; 3 half-windows of 128 -- 84 %); stream_windows 1 keeps whole windows
+        int hsw = 0;
+        const int nh = (a.st_nsegs >= 2 || d->stream_windows == 2) ? stream_segments(a.W, a.ldw, d->n_tv, &hsw, TV_COLS / 2) : 0;
+        if (nh > 0 && (d->stream_windows == 2 || (d->stream_windows == 0 &&
+            (double)a.W / (nh * (TV_COLS / 2)) > (double)a.W / (a.st_nsegs * TV_COLS) + 0.1))) {
+            a.st_half = 1;
+            a.st_nsegs = nh;
+            a.st_seg_w = hsw;
+            a.st_nvp = (d->B * d->C * nh + 1) / 2;
+        }
+        if (choose_split((long long)a.st_nvp, d->H, d->n_tv, d->stream_wgs, &a.split_wgs)) {
             g_sel_err = g_err;
             return -1;
         }

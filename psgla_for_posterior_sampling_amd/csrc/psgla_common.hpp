@@ -123,6 +123,9 @@ struct TvArgs {
     int stream;                     // 1: main pass = row-streaming pipeline kernel
     int split_wgs;                  // stream kernel: > 0 = row-split mode over this many workgroups
     int st_nsegs, st_seg_w, st_halo;  // stream kernel column segmentation (W > 256)
+    int st_half;                    // stream kernel: 1 = half windows (two 128-column segments per wave, one per
+                                    // half-wave; 256 < W <= 324 at n_tv = 10: a third of the lanes fewer idle)
+    int st_nvp;                     // stream kernel virtual planes: (plane, segment) items, or pairs of them (st_half)
     int fin_inline;                 // stream kernel: 1 = the last workgroup finalises the step
     int tile_r;                     // > 0: small-batch tile kernel with tile_r rows per wave (one tile per workgroup)
     int tile_nw;                    // tile kernel: waves per workgroup (16 or 8)
@@ -299,7 +302,7 @@ constexpr int tile_mst_rows(int nw, int r) { return nw * r < 56 ? nw * r : 56; }
 // kernel launchers (one translation unit each)
 template <bool EXACT, int FRONT, bool ALPHA1> void launch_band_main(const TvArgs& a, dim3 grid, hipStream_t st);
 template <bool EXACT, int FRONT, bool ALPHA1> void launch_band_finalise(const TvArgs& a, dim3 grid, hipStream_t st);
-void launch_stream(const TvArgs& a, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen);
+void launch_stream(const TvArgs& a, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen, bool half);
 bool launch_tile(const TvArgs& a, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen);
 
 }  // namespace psgla

@@ -47,7 +47,7 @@ struct StreamSharedT {
     float4 fsy[SP_FRONT][A1 ? 2 : 1][WAVE];
     uint32_t fmk[SP_FRONT][2][WAVE];
     float4 bst[SP_BACK][2][2][WAVE];
-    float red[SP_MAXSEG][SP_MAXST][2];
+    float red[SP_MAXSEG][2][SP_MAXST][2];   // rel-err partial sums per (stream segment, half-wave, iteration)
     // ring holding the output of stage k (k = 0: the front's ring 0, !A1 only)
     static __device__ __forceinline__ constexpr int rk(int k) { return A1 ? k - 1 : k; }
     __device__ __forceinline__ float4* stX(int fw, int q) { return A1 ? &fsx[fw][((q >> 2) % 3)][0][0] : &fsx[fw][(q >> 2) & 1][0][0]; }
@@ -86,10 +86,10 @@ __device__ __forceinline__ void build_rowmap(const TvArgs& a, int wg, RowMap& m)
     if (a.split_wgs <= 0) {
         m.ns = 1; m.Q = H; m.htop = 0; m.hbot = 0;
         m.q1 = m.q2 = m.q3 = H;
-        m.pl0 = wg;                   // virtual plane (plane * st_nsegs + column segment)
+        m.pl0 = wg;                   // virtual plane (plane * st_nsegs + column segment, or a pair of them)
         return;
     }
-    const long long T = (long long)a.B * a.C * a.st_nsegs * H;
+    const long long T = (long long)a.st_nvp * H;
     const long long g0 = T * wg / a.split_wgs, g1 = T * (wg + 1) / a.split_wgs;
     const int p0 = (int)(g0 / H), p1 = (int)((g1 - 1) / H);
     const int h = a.n_tv;
@@ -127,27 +127,45 @@ __device__ __forceinline__ void plane_rowmap(int H, int plane, RowMap& m) {
     m.lo0 = m.lo1 = m.lo2 = m.lo3 = 0;
 }
 
-// Column geometry of a virtual plane vp = plane * st_nsegs + segment: the real plane, the start of the
-// segment's 256-column wave window (f0) and its core columns [cc0, cc1).  Without GEN there is one
-// segment (vp = plane, the whole row).
+// Column geometry of a virtual plane: the real plane, the start of the segment's wave window (f0) and its core
+// columns [cc0, cc1).  Without GEN there is one segment (vp = plane, the whole row).  GEN: vp = item = plane *
+// st_nsegs + column segment, a 256-column window.  HALF (st_half): vp is a PAIR of items, 2 vp + h in half-wave h
+// (lanes 32 h .. 32 h + 31, a 128-column window each); a pair's missing second item (odd item count) repeats the
+// first in a disabled half (on = false: nothing stored or counted there); vp >= st_nvp -- the early-stop
+// recompute -- is item vp - st_nvp in both halves.  h: the lane's half (HALF only, per lane).
 struct SegGeo {
     int rp, f0, cc0, cc1;
+    bool on;
 };
-template <bool GEN>
-__device__ __forceinline__ SegGeo seg_geo(const TvArgs& a, int vp) {
+template <bool GEN, bool HALF = false>
+__device__ __forceinline__ SegGeo seg_geo(const TvArgs& a, int vp, int h = 0) {
     SegGeo g;
+    g.on = true;
     if (!GEN) {
         g.rp = vp; g.f0 = 0; g.cc0 = 0; g.cc1 = a.W;
         return g;
     }
+    int item = vp;
+    if (HALF) {
+        const int nitems = a.B * a.C * a.st_nsegs;
+        if (vp >= a.st_nvp) {
+            item = vp - a.st_nvp;
+        } else {
+            item = 2 * vp + h;
+            if (item >= nitems) { item = 2 * vp; g.on = false; }
+        }
+    }
     const int ns = a.st_nsegs;
-    g.rp = vp / ns;
-    const int sgi = vp - g.rp * ns;
+    g.rp = item / ns;
+    const int sgi = item - g.rp * ns;
     g.cc0 = sgi * a.st_seg_w;
-    g.cc1 = min(a.W, g.cc0 + a.st_seg_w);
+    g.cc1 = (sgi == ns - 1) ? a.W : min(a.W, g.cc0 + a.st_seg_w);   // the last segment takes the rest
     g.f0 = max(0, g.cc0 - a.st_halo) & ~3;
     return g;
 }
+// a lane's position in its window: HALF windows are half-waves
+template <bool HALF>
+__device__ __forceinline__ int lcol(int lane) { return HALF ? (lane & 31) : lane; }
 
 // Position of a role's current row in the stream; advanced monotonically (the segment walk
 // runs only when a plane boundary is crossed).
@@ -163,14 +181,15 @@ struct RowGeo {
     int bb;             // chain (batch entry)
     int f0;             // first column of the wave window (GEN; 0 otherwise)
     int cc0, cc1;       // core columns of the segment
+    bool on;            // HALF: the lane's half-window holds an item
 };
 struct RowCursor {
     int q, s, p, r, qend;
     RowGeo g;
 };
-template <bool GEN>
+template <bool GEN, bool HALF>
 __device__ __forceinline__ RowGeo row_geo(const TvArgs& a, int vp) {
-    const SegGeo sg = seg_geo<GEN>(a, vp);
+    const SegGeo sg = seg_geo<GEN, HALF>(a, vp, HALF ? (int)((threadIdx.x & 63) >> 5) : 0);
     const size_t HW = (size_t)a.H * a.ldw;
     RowGeo g;
     g.bb = sg.rp / a.C;
@@ -182,25 +201,26 @@ __device__ __forceinline__ RowGeo row_geo(const TvArgs& a, int vp) {
     g.f0 = sg.f0;
     g.cc0 = sg.cc0;
     g.cc1 = sg.cc1;
+    g.on = sg.on;
     return g;
 }
-template <bool GEN>
+template <bool GEN, bool HALF>
 __device__ __forceinline__ void cursor_seek(const TvArgs& a, const RowMap& m, RowCursor& c) {
     while (c.s + 1 < m.ns && c.q >= m.qs(c.s + 1)) ++c.s;
     c.qend = m.qs(c.s + 1);
     c.p = m.pl(c.s);
     c.r = m.lo(c.s) + (c.q - m.qs(c.s));
-    c.g = row_geo<GEN>(a, c.p);
+    c.g = row_geo<GEN, HALF>(a, c.p);
 }
-template <bool GEN>
+template <bool GEN, bool HALF>
 __device__ __forceinline__ void cursor_init(const TvArgs& a, const RowMap& m, RowCursor& c, int q) {
     c.q = q; c.s = 0;
-    cursor_seek<GEN>(a, m, c);
+    cursor_seek<GEN, HALF>(a, m, c);
 }
-template <bool GEN>
+template <bool GEN, bool HALF>
 __device__ __forceinline__ void cursor_advance(const TvArgs& a, const RowMap& m, RowCursor& c, int d) {
     c.q += d; c.r += d;
-    if (c.q >= c.qend && c.s + 1 < m.ns) cursor_seek<GEN>(a, m, c);
+    if (c.q >= c.qend && c.s + 1 < m.ns) cursor_seek<GEN, HALF>(a, m, c);
 }
 // stream index of the first segment start after stream row q (SP_NOSEG if none)
 __device__ __forceinline__ int next_seg_start(const RowMap& m, int q) {
@@ -213,6 +233,11 @@ __device__ __forceinline__ int next_seg_start(const RowMap& m, int q) {
 // One pipeline stage = one inner TV iteration on one row pair.  Phase A (primal) on the
 // lookahead row j from ring k-1; phase B (dual) on the output row i = j-1, which needs z of
 // rows i (held from the previous step) and j.
+// per-component select of two float4 (a ternary on the structs is lowered through a scratch copy)
+__device__ __forceinline__ float4 sel4(bool c, const float4& x, const float4& y) {
+    return make_float4(c ? x.x : y.x, c ? x.y : y.y, c ? x.z : y.z, c ? x.w : y.w);
+}
+
 struct StageRow {
     float u0[CPL], u1[CPL];   // u2^{k-1} of the row
     float z[CPL];             // z^k of the row
@@ -220,7 +245,7 @@ struct StageRow {
     int lk;                   // GEN: the row's lastk (its column segment's), set by the primal
 };
 
-template <bool EXACT, bool TRK, bool GEN = false>
+template <bool EXACT, bool TRK, bool GEN = false, bool HALF = false>
 __device__ __forceinline__ void stage_phase_a(const TvArgs& a, const float4& X2, const float4& U0,
                                               const float4& U1, const float4& YY, const float (&pu0)[CPL],
                                               StageRow& o, float& sd, float& sn, int nreal = CPL) {
@@ -229,8 +254,10 @@ __device__ __forceinline__ void stage_phase_a(const TvArgs& a, const float4& X2,
     o.u0[0] = U0.x; o.u0[1] = U0.y; o.u0[2] = U0.z; o.u0[3] = U0.w;
     o.u1[0] = U1.x; o.u1[1] = U1.y; o.u1[2] = U1.z; o.u1[3] = U1.w;
     // u1 of the column left of this lane's first column (lane-1's last); 0 at lane 0
-    const float u1l = __int_as_float(
+    float u1l = __int_as_float(
         __builtin_amdgcn_update_dpp(0, __float_as_int(o.u1[CPL - 1]), 0x138 /* wave_shr:1 */, 0xF, 0xF, true));
+    // HALF: lane 32 starts a window (the image's left edge or a halo cut: 0 either way)
+    if (HALF && (threadIdx.x & 63) == 32) u1l = 0.f;
 #pragma unroll
     for (int kk = 0; kk < CPL; ++kk) {
         const float u1left = kk > 0 ? o.u1[kk - 1] : u1l;
@@ -319,19 +346,19 @@ __device__ __forceinline__ void stage_phase_b(const TvArgs& a, const StageRow& r
 // FIRST (A1 only): stage 1, which reads its input row straight from the front's DMA staging (the row's front
 // wave j % 4, slot (j / 4) % 3) instead of a ring -- a separate instantiation, so no stage branches on k around
 // its LDS reads.
-template <bool EXACT, bool TRK, bool GEN, bool A1, bool FIRST>
+template <bool EXACT, bool TRK, bool GEN, bool A1, bool FIRST, bool HALF>
 __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamSharedT<A1>& sh, const RowMap& rm, int k, int n,
-                                           int nsteps, int Qk, int lane, int lastk, int nreal, bool core) {
+                                           int nsteps, int Qk, int lane, int lastk, int nreal, bool core, bool fresh) {
     // GEN: the lane's columns change with the column segment of the row (row split over virtual
     // planes): lastk / nreal / core follow the primal row's segment; each row carries its lastk
     // to its dual (StageRow.lk)
     auto set_geo = [&](int sgi) {
         if (GEN) {
-            const SegGeo g = seg_geo<GEN>(a, rm.pl(sgi));
-            const int gj = g.f0 + CPL * lane;
+            const SegGeo g = seg_geo<GEN, HALF>(a, rm.pl(sgi), lane >> 5);
+            const int gj = g.f0 + CPL * lcol<HALF>(lane);
             lastk = a.W - 1 - gj;
             nreal = min(CPL, max(0, a.W - gj));
-            core = gj < a.W && gj >= g.cc0 && gj < g.cc1;
+            core = g.on && gj < a.W && gj >= g.cc0 && gj < g.cc1;
         }
     };
     const int Q = Qk;                    // rows this stage runs (the stream's, bottom-halo trimmed)
@@ -345,17 +372,31 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamSharedT<A1>& s
     const int qc0 = rm.htop, qc1 = Q - rm.hbot;   // core stream rows
     auto flush = [&]() {
         if (TRK) {
-            float d = wave_sum(core ? lsd : 0.f);
-            const float q = wave_sum(core ? lsn : 0.f);
-            if (!EXACT) d *= a.rho * a.rho;          // fast sums hold (x - x2_prev)^2
-            if (lane == 0) { sh.red[sacc][k - 1][0] = d; sh.red[sacc][k - 1][1] = q; }
+            if (HALF) {                              // one sum per half-wave (each its own item / chain)
+                const float2 rs = row_sum2(core ? lsd : 0.f, core ? lsn : 0.f);
+                const int xi = __float_as_int(rs.x), yi = __float_as_int(rs.y);
+                float d0 = __int_as_float(__builtin_amdgcn_readlane(xi, 0)) + __int_as_float(__builtin_amdgcn_readlane(xi, 16));
+                float d1 = __int_as_float(__builtin_amdgcn_readlane(xi, 32)) + __int_as_float(__builtin_amdgcn_readlane(xi, 48));
+                const float q0 = __int_as_float(__builtin_amdgcn_readlane(yi, 0)) + __int_as_float(__builtin_amdgcn_readlane(yi, 16));
+                const float q1 = __int_as_float(__builtin_amdgcn_readlane(yi, 32)) + __int_as_float(__builtin_amdgcn_readlane(yi, 48));
+                if (!EXACT) { d0 *= a.rho * a.rho; d1 *= a.rho * a.rho; }
+                if (lane == 0) {
+                    sh.red[sacc][0][k - 1][0] = d0; sh.red[sacc][0][k - 1][1] = q0;
+                    sh.red[sacc][1][k - 1][0] = d1; sh.red[sacc][1][k - 1][1] = q1;
+                }
+            } else {
+                float d = wave_sum(core ? lsd : 0.f);
+                const float q = wave_sum(core ? lsn : 0.f);
+                if (!EXACT) d *= a.rho * a.rho;          // fast sums hold (x - x2_prev)^2
+                if (lane == 0) { sh.red[sacc][0][k - 1][0] = d; sh.red[sacc][0][k - 1][1] = q; }
+            }
             lsd = 0.f; lsn = 0.f;
         }
     };
     auto primal = [&](int j, const float4& X2, const float4& U0, const float4& U1, const float4& YY,
                       const float (&pu0)[CPL], StageRow& cur) {
         float rd = 0.f, rn = 0.f;
-        stage_phase_a<EXACT, TRK, GEN>(a, X2, U0, U1, YY, pu0, cur, rd, rn, nreal);
+        stage_phase_a<EXACT, TRK, GEN, HALF>(a, X2, U0, U1, YY, pu0, cur, rd, rn, nreal);
         if (GEN) cur.lk = lastk;
         if (TRK && j >= qc0 && j < qc1) { lsd += rd; lsn += rn; }
     };
@@ -364,17 +405,23 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamSharedT<A1>& s
     const int rin = StreamSharedT<A1>::rk(k - 1), rout = StreamSharedT<A1>::rk(k);
     auto load_row = [&](int j, float4& X2, float4& U0, float4& U1, float4& YY) {
         float4 A, B;
+        YY = sh.y[j & (SP_YRING - 1)][lane];
         if (FIRST) {
-            X2 = sh.stX(j & 3, j)[lane];
-            A = sh.stUa(j & 3, j)[lane];
-            B = sh.stUb(j & 3, j)[lane];
+            // the front's staging of row j (x2 = X, u2); a TV restart (fresh): x2 = Y, u2 = 0 (selects, no branch
+            // around the LDS reads; lanes beyond the image read DMA'd values: they never feed an image column)
+            const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 sX = sh.stX(j & 3, j)[lane];
+            const float4 sA = sh.stUa(j & 3, j)[lane];
+            const float4 sB = sh.stUb(j & 3, j)[lane];
+            X2 = sel4(fresh, YY, sX);
+            A = sel4(fresh, zero4, sA);
+            B = sel4(fresh, zero4, sB);
         } else {
             const int sl = j & 1;
             X2 = sh.x2[rin][sl][lane];
             A = sh.ua[rin][sl][lane];
             B = sh.ub[rin][sl][lane];
         }
-        YY = sh.y[j & (SP_YRING - 1)][lane];
         U0 = make_float4(A.x, A.z, B.x, B.z);
         U1 = make_float4(A.y, A.w, B.y, B.w);
     };
@@ -455,7 +502,7 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamSharedT<A1>& s
 // pass and the rare early-stop recompute, each with its own register allocation.
 // GEN: the row pitch is not the image width (rows padded: W % 4 != 0) -- the last-column, norm
 // and noise-window handling of such rows, compiled only into the kernels that need it
-template <bool EXACT, bool ALPHA1, bool GEN>
+template <bool EXACT, bool ALPHA1, bool GEN, bool HALF>
 __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA1>& sh, const RowMap& rm, const int n,
                                             const bool track, const long long step, const bool fresh) {
     const int lane = threadIdx.x & (WAVE - 1);
@@ -470,10 +517,11 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
     const int Q = rm.Q;
     const int qc0 = rm.htop, qc1 = Q - rm.hbot;          // core stream rows
     // column geometry of the first row's segment (the only one without GEN)
-    const SegGeo g0 = seg_geo<GEN>(a, rm.pl0);
+    const SegGeo g0 = seg_geo<GEN, HALF>(a, rm.pl0, lane >> 5);
     const int cc0 = g0.cc0, cc1 = g0.cc1;
-    const int gj0 = g0.f0 + CPL * lane;
-    const bool lane_ok = gj0 < W;
+    const int lc = lcol<HALF>(lane);
+    const int gj0 = g0.f0 + CPL * lc;
+    const bool lane_ok = g0.on && gj0 < W;
     const bool core = lane_ok && gj0 >= cc0 && gj0 < cc1;   // a lane's 4 columns are all core or none
     // Bottom-halo trim (split mode): the stream's last row is an artificial edge, so stage k's
     // output is exact down to one row less than its input's; the core rows (< Qb) only need
@@ -507,13 +555,13 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
         // per front wave), row and column clamped into the plane so every lane loads.
         const int gjc = min(gj0, L - CPL);
         RowCursor rc_cur, rc_dma;
-        cursor_init<GEN>(a, rm, rc_cur, min(fw, Q - 1));
-        cursor_init<GEN>(a, rm, rc_dma, min(fw, Q - 1));
+        cursor_init<GEN, HALF>(a, rm, rc_cur, min(fw, Q - 1));
+        cursor_init<GEN, HALF>(a, rm, rc_dma, min(fw, Q - 1));
         // part `part` of the loads of stream row q: 0 = X, 1 = y, 2 = u2 (two halves), 3 = mask (+ x2)
         auto front_issue = [&](int part, int q, const RowCursor& rc) {
             const int rr = min(rc.r, H - 1);
             const int bi = (q >> 2) & 1;
-            const int gjr = GEN ? min(rc.g.f0 + CPL * lane, L - CPL) : gjc;
+            const int gjr = GEN ? min(rc.g.f0 + CPL * lc, L - CPL) : gjc;
             // 64-bit per-lane addresses (the SGPR-base form measured +12 % in round 2:
             // this kernel's row cursor sits in VGPRs, so each DMA pays two readfirstlane + 5 wait states)
             const size_t roff = (size_t)rr * L + gjr;
@@ -534,7 +582,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
         // phase of row q (into the buffer of row q - 4, consumed before phase 0 of row q), so
         // their issue cost is spread over four steps
         for (int part = 0; part < 4; ++part) front_issue(part, fw, rc_dma);
-        cursor_advance<GEN>(a, rm, rc_dma, min(4, max(0, Q - 1 - fw)));
+        cursor_advance<GEN, HALF>(a, rm, rc_dma, min(4, max(0, Q - 1 - fw)));
         // ======================= FRONT =======================
         // Row q (q % 4 == fw) runs its four phases in steps q .. q + 3: the loop below is unrolled by
         // phase (one step barrier after each), so no step decides its phase at run time.
@@ -546,8 +594,8 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
             {
                 const RowGeo& g = rc_cur.g;
                 if (GEN) {                                  // this row's segment's lanes
-                    gjf = g.f0 + CPL * lane;
-                    okf = gjf < W;
+                    gjf = g.f0 + CPL * lc;
+                    okf = g.on && gjf < W;
                 }
                 // element index in the chain's unpadded C*H*W image: the noise stream
                 // does not depend on the row pitch
@@ -608,27 +656,22 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
                     }
                 }
                 const float4 Y4 = make_float4(Yv[0], Yv[1], Yv[2], Yv[3]);
-                if (ALPHA1) {
-                    // stage 1 reads x2 = X and u2 from this staging; a TV restart (fresh) makes them Y and 0
-                    // (lanes beyond the image keep the DMA'd values: they never feed an image column)
-                    if (fresh) {
-                        sh.stX(fw, q)[lane] = okf ? Y4 : zero4;
-                        sh.stUa(fw, q)[lane] = zero4;
-                        sh.stUb(fw, q)[lane] = zero4;
-                    }
-                } else {
-                    float4 x2s = fresh ? Y4 : sh.stX2(fw, q)[lane];
-                    if (!okf) x2s = zero4;
+                if (!ALPHA1) {
+                    // ring 0 = (x2, u2) of the staging; a TV restart (fresh): Y and 0 (reads first, then selects)
+                    const float4 sX2 = sh.stX2(fw, q)[lane];
+                    const float4 sA = sh.stUa(fw, q)[lane];
+                    const float4 sB = sh.stUb(fw, q)[lane];
+                    const float4 x2s = sel4(okf, sel4(fresh, Y4, sX2), zero4);
                     const int s0 = q & 1;
                     sh.x2[0][s0][lane] = x2s;
-                    sh.ua[0][s0][lane] = fresh ? zero4 : sh.stUa(fw, q)[lane];
-                    sh.ub[0][s0][lane] = fresh ? zero4 : sh.stUb(fw, q)[lane];
+                    sh.ua[0][s0][lane] = sel4(fresh, zero4, sA);
+                    sh.ub[0][s0][lane] = sel4(fresh, zero4, sB);
                 }
                 sh.y[q & (SP_YRING - 1)][lane] = Y4;
                 // the wave's next rows: noise row q + 4, DMA of row q + 8... issued as q + 4
                 front_issue(3, q + 4, rc_dma);
-                cursor_advance<GEN>(a, rm, rc_cur, 4);
-                if (q + 8 < Q) cursor_advance<GEN>(a, rm, rc_dma, 4);
+                cursor_advance<GEN, HALF>(a, rm, rc_cur, 4);
+                if (q + 8 < Q) cursor_advance<GEN, HALF>(a, rm, rc_dma, 4);
             }
             step_barrier();
             t += 4;
@@ -643,9 +686,9 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
         const int nreal = min(CPL, max(0, W - gj0));      // real (non-pitch-padding) columns of the lane
         __builtin_amdgcn_s_setprio(1);
         const int qk = stage_rows(k_st);
-        if (ALPHA1 && k_st == 1) stage_loop<EXACT, false, GEN, ALPHA1, true>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core);
-        else if (trk) stage_loop<EXACT, true, GEN, ALPHA1, false>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core);
-        else stage_loop<EXACT, false, GEN, ALPHA1, false>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core);
+        if (ALPHA1 && k_st == 1) stage_loop<EXACT, false, GEN, ALPHA1, true, HALF>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core, fresh);
+        else if (trk) stage_loop<EXACT, true, GEN, ALPHA1, false, HALF>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core, fresh);
+        else stage_loop<EXACT, false, GEN, ALPHA1, false, HALF>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core, fresh);
     } else if (role == 3) {
         for (int t = 0; t < nsteps; ++t) step_barrier();
     } else {
@@ -661,13 +704,13 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
         const bool need_prev = si.acc && !si.first;
         const int gjc = min(gj0, L - CPL);
         RowCursor rc_cur, rc_dma;
-        cursor_init<GEN>(a, rm, rc_cur, min(bw, Q - 1));
-        cursor_init<GEN>(a, rm, rc_dma, min(bw, Q - 1));
+        cursor_init<GEN, HALF>(a, rm, rc_cur, min(bw, Q - 1));
+        cursor_init<GEN, HALF>(a, rm, rc_dma, min(bw, Q - 1));
         auto back_issue = [&](int q, const RowCursor& rc) {
             if (need_prev) {
                 const int rr = min(rc.r, H - 1);
                 const int bi = (q >> 1) & 1;
-                const int gjr = GEN ? min(rc.g.f0 + CPL * lane, L - CPL) : gjc;
+                const int gjr = GEN ? min(rc.g.f0 + CPL * lc, L - CPL) : gjc;
                 const size_t base = rc.g.pbase + (size_t)rr * L + gjr;
                 glds16(mean_in + base, &sh.bst[bw][bi][0][0]);
                 glds16(sq_in + base, &sh.bst[bw][bi][1][0]);
@@ -695,7 +738,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
         // mean / sq rows are LDS-DMA'd two of the wave's rows ahead (4 stream rows); c1 / c2 =
         // vector-memory ops issued after the DMA of the wave's next / next-but-one row
         back_issue(bw, rc_dma);
-        if (bw + 2 < Q) cursor_advance<GEN>(a, rm, rc_dma, 2);
+        if (bw + 2 < Q) cursor_advance<GEN, HALF>(a, rm, rc_dma, 2);
         back_issue(bw + 2, rc_dma);
         int c1 = 2, c2 = 0;
         // ======================= BACK =======================
@@ -751,8 +794,8 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
                 // buffer is re-targeted by the next DMA
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 const RowCursor rc = rc_cur;
-                cursor_advance<GEN>(a, rm, rc_cur, 2);
-                if (q + 4 < Q) cursor_advance<GEN>(a, rm, rc_dma, 2);
+                cursor_advance<GEN, HALF>(a, rm, rc_cur, 2);
+                if (q + 4 < Q) cursor_advance<GEN, HALF>(a, rm, rc_dma, 2);
                 back_issue(q + 4, rc_dma);   // into the buffer just consumed (rows q, q + 4 share it)
                 asm volatile("" ::: "memory");
                 const bool rowcore = q >= qc0 && q < qc1;
@@ -762,8 +805,8 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
                     c2 = ns;
                 }
                 // GEN: the lanes' columns of this row's segment
-                const int gjr = GEN ? rc.g.f0 + CPL * lane : gj0;
-                const bool corer = GEN ? (gjr < W && gjr >= rc.g.cc0 && gjr < rc.g.cc1) : core;
+                const int gjr = GEN ? rc.g.f0 + CPL * lc : gj0;
+                const bool corer = GEN ? (rc.g.on && gjr < W && gjr >= rc.g.cc0 && gjr < rc.g.cc1) : core;
                 if (rowcore && corer) {
                     const size_t base = rc.g.pbase + (size_t)rc.r * L + gjr;
                     st_nt(a.x[par_out] + base, Xo);
@@ -796,7 +839,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
     // early-stop test, per chain); the tracking stages wrote sh.red[segment][k - 1]
 }
 
-template <bool EXACT, bool ALPHA1, bool GEN>
+template <bool EXACT, bool ALPHA1, bool GEN, bool HALF>
 __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     __shared__ StreamSharedT<ALPHA1> sh;
     __shared__ int s_stop[MAXG];
@@ -807,18 +850,25 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     {
         RowMap rm;
         build_rowmap(a, blockIdx.x, rm);
-        stream_pass<EXACT, ALPHA1, GEN>(a, sh, rm, a.n_tv, true, step, fresh);
+        stream_pass<EXACT, ALPHA1, GEN, HALF>(a, sh, rm, a.n_tv, true, step, fresh);
         if (!a.fin_inline) return;        // main-pass-only launch (kernel timing): no side effects
         // rel_err partial sums of this stream -> global, per segment's chain (deepinv's
         // early-stop test, per chain); the tracking stages wrote sh.red[segment][k - 1]
         lds_barrier();
-        for (int tt = threadIdx.x; tt < SP_MAXSEG * SP_MAXST; tt += blockDim.x) {
-            const int sg = tt / SP_MAXST, it = tt - sg * SP_MAXST;     // it = k - 1
-            if (sg < rm.ns && it >= 2 && it <= a.n_tv - 2) {
-                const int pl = rm.pl(sg) / a.st_nsegs;        // virtual plane -> plane
+        for (int tt = threadIdx.x; tt < SP_MAXSEG * 2 * SP_MAXST; tt += blockDim.x) {
+            const int sg = tt / (2 * SP_MAXST), hh = (tt / SP_MAXST) & 1, it = tt % SP_MAXST;   // it = k - 1
+            if (sg < rm.ns && (HALF || hh == 0) && it >= 2 && it <= a.n_tv - 2) {
+                // virtual plane -> item -> plane (HALF: the half-wave's item; a disabled half has none)
+                const int vp = rm.pl(sg);
+                int item = vp;
+                if (HALF) {
+                    item = 2 * vp + hh;
+                    if (item >= a.B * C * a.st_nsegs) continue;
+                }
+                const int pl = item / a.st_nsegs;
                 const int g = a.per_chain_norm ? pl / C : 0;
-                atomicAdd(&a.norms[((size_t)g * a.n_tv + it) * 2], (double)sh.red[sg][it][0]);
-                atomicAdd(&a.norms[((size_t)g * a.n_tv + it) * 2 + 1], (double)sh.red[sg][it][1]);
+                atomicAdd(&a.norms[((size_t)g * a.n_tv + it) * 2], (double)sh.red[sg][hh][it][0]);
+                atomicAdd(&a.norms[((size_t)g * a.n_tv + it) * 2 + 1], (double)sh.red[sg][hh][it][1]);
             }
         }
     }
@@ -878,9 +928,10 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
         if (item < 0) break;
         const int plane = item / a.st_nsegs;
         RowMap rm;
-        plane_rowmap(a.H, item, rm);                 // the virtual plane (plane, column segment)
+        // the virtual plane (plane, column segment); HALF: the item alone, in both half-waves
+        plane_rowmap(a.H, HALF ? a.st_nvp + item : item, rm);
         const int nstop = __builtin_amdgcn_readfirstlane(s_stop[plane / C]);
-        stream_pass<EXACT, ALPHA1, GEN>(a, sh, rm, nstop, false, step, fresh);
+        stream_pass<EXACT, ALPHA1, GEN, HALF>(a, sh, rm, nstop, false, step, fresh);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < a.B * a.n_tv * 2; i += blockDim.x) a.norms[i] = 0.0;
@@ -891,11 +942,12 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     }
 }
 
-void launch_stream(const TvArgs& s, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen) {
-#define PSGLA_STREAM(E, A, G) \
-    if (exact == E && alpha1 == A && gen == G) { hipLaunchKernelGGL((tv_stream_kernel<E, A, G>), grid, dim3(TV_THREADS), 0, st, s); return; }
-    PSGLA_STREAM(true, true, false) PSGLA_STREAM(true, true, true) PSGLA_STREAM(true, false, false) PSGLA_STREAM(true, false, true)
-    PSGLA_STREAM(false, true, false) PSGLA_STREAM(false, true, true) PSGLA_STREAM(false, false, false) PSGLA_STREAM(false, false, true)
+void launch_stream(const TvArgs& s, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen, bool half) {
+#define PSGLA_STREAM(E, A, G, HF) \
+    if (exact == E && alpha1 == A && gen == G && half == HF) { hipLaunchKernelGGL((tv_stream_kernel<E, A, G, HF>), grid, dim3(TV_THREADS), 0, st, s); return; }
+    PSGLA_STREAM(true, true, false, false) PSGLA_STREAM(true, true, true, false) PSGLA_STREAM(true, false, false, false) PSGLA_STREAM(true, false, true, false)
+    PSGLA_STREAM(false, true, false, false) PSGLA_STREAM(false, true, true, false) PSGLA_STREAM(false, false, false, false) PSGLA_STREAM(false, false, true, false)
+    PSGLA_STREAM(true, true, true, true) PSGLA_STREAM(true, false, true, true) PSGLA_STREAM(false, true, true, true) PSGLA_STREAM(false, false, true, true)
 #undef PSGLA_STREAM
 }
 

@@ -49,7 +49,7 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
     const int e0 = max(0, r0 - h), e1 = min(H, r1 + h);
     // column window of the segment: core columns [cc0, cc1), wave window [f0, f0 + 256)
     const int cc0 = GEN ? seg * a.st_seg_w : 0;
-    const int cc1 = GEN ? min(W, cc0 + a.st_seg_w) : W;
+    const int cc1 = GEN ? (seg == a.st_nsegs - 1 ? W : min(W, cc0 + a.st_seg_w)) : W;   // the last segment: the rest
     const int f0 = GEN ? (max(0, cc0 - a.st_halo) & ~3) : 0;
     const int gj0 = f0 + CPL * lane;
     const int gjc = min(gj0, L - CPL);                 // DMA source column (every lane in bounds)
@@ -355,8 +355,11 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
             const float4 B4 = make_float4(Bs[0], Bs[1], Bs[2], Bs[3]);
             float* const pa = u2r + 2 * gj0;                     // own A
             float* const pb = u2r + 2 * gjo + 4;                 // the other lane's B
-            if (lo ? corelane : corelane_o) st_tile(lo ? pa : pb, lo ? A : B4);
-            if (lo ? corelane_o : corelane) st_tile(lo ? pb : pa, lo ? B4 : A);
+            // (per-component selects: a ternary on the float4 structs is lowered through a scratch copy)
+            const float4 v1 = make_float4(lo ? A.x : B4.x, lo ? A.y : B4.y, lo ? A.z : B4.z, lo ? A.w : B4.w);
+            const float4 v2 = make_float4(lo ? B4.x : A.x, lo ? B4.y : A.y, lo ? B4.z : A.z, lo ? B4.w : A.w);
+            if (lo ? corelane : corelane_o) st_tile(lo ? pa : pb, v1);
+            if (lo ? corelane_o : corelane) st_tile(lo ? pb : pa, v2);
         }
     }
 }

@@ -29,7 +29,7 @@ class FusedTvChains:
                  n_inter: int, n_inter_mmse: int, chain0: int = 0, exact: bool = False,
                  tv_x2: torch.Tensor | None = None, tv_u2: torch.Tensor | None = None,
                  store_samples: bool = True, store_blocks: bool = True, kernel_variant: str = "auto",
-                 stream_wgs: int = 0):
+                 stream_wgs: int = 0, stream_windows: str = "auto"):
         if init.dim() != 4:
             raise ValueError("init must be (B, C, H, W)")
         if tv.n_it > N.TV_MAX_FUSED_IT:
@@ -99,6 +99,9 @@ class FusedTvChains:
         d.arrive = self.work.arrive.data_ptr()
         d.kernel_variant = KERNEL_VARIANTS[kernel_variant]
         d.stream_wgs = int(stream_wgs)
+        if stream_windows not in ("auto", "whole", "half"):
+            raise ValueError("stream_windows must be 'auto', 'whole' or 'half'")
+        d.stream_windows = {"auto": 0, "whole": 1, "half": 2}[stream_windows]
         self.desc = d
         self.sched_struct = self.sched.struct(True, 0)
         if self.warm_first:

@@ -640,12 +640,15 @@ def test_generic_psgla_deblur_matches_reference_fixture(bt):
     assert rel(M2l.mean(0), fx["blocks2"].mean(0)) < REL_TOL_MEAN
 
 
-@pytest.mark.parametrize("H,W,alpha", [(23, 29, 1.0), (19, 31, 1.0), (21, 33, 0.6), (16, 61, 1.0), (13, 301, 1.0),
-                                       (11, 483, 1.0)])
-def test_stream_padded_rows_exact_vs_oracle(H, W, alpha):
+@pytest.mark.parametrize("B,H,W,alpha", [(2, 23, 29, 1.0), (2, 19, 31, 1.0), (2, 21, 33, 0.6), (2, 16, 61, 1.0),
+                                         (2, 13, 301, 1.0), (2, 11, 483, 1.0),
+                                         # half-wave windows (256 < W <= 324): 3 segments of <= 128 columns, two per
+                                         # wave; B = 1: 9 segments, the last pair's second half disabled
+                                         (1, 17, 321, 1.0), (2, 15, 290, 0.6)])
+def test_stream_padded_rows_exact_vs_oracle(B, H, W, alpha):
     """W % 4 != 0 (rows padded to a multiple of 4 columns, the lane's 4 noise elements spanning two
-    quads at every offset) and W > 256 (column segments): the streaming kernel, bit-identical."""
-    B = 2
+    quads at every offset) and W > 256 (column segments; for 256 < W <= 324 half-wave windows, a pair of
+    segments per wave): the streaming kernel, bit-identical."""
     eng, (dg, y, init, mask2d, c1, c2) = _fused_batch(B, 5, exact=True, n_iter=12, H=H, W=W, alpha=alpha,
                                                       variant="stream")
     assert eng.main_kernel == "tv_stream_kernel"

@@ -47,20 +47,22 @@ __device__ __forceinline__ void diag_barrier(SH& sh) {
 }
 '''
 import os as _os
-_N_BARRIER = open(_os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "..", "..", "psgla_for_posterior_sampling_amd",
-                                "csrc", "tv_stream.hip")).read().count("step_barrier();")
+_SRC = open(_os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "..", "..", "psgla_for_posterior_sampling_amd",
+                          "csrc", "tv_stream.hip")).read()
+_N_BARRIER = _SRC.count("step_barrier();")
+_SP = "HALF>" if "stream_pass<EXACT, ALPHA1, GEN, HALF>(a, sh, rm, a.n_tv" in _SRC else ">"
 PATCHES = [
     ("template <bool A1>\nstruct StreamSharedT {\n", DIAG + "template <bool A1>\nstruct StreamSharedT {\n", 1),
-    ("    float red[SP_MAXSEG][SP_MAXST][2];\n", "    float red[SP_MAXSEG][SP_MAXST][2];\n    StepDiag sd;\n", 1),
+    ("    float red[SP_MAXSEG][2][SP_MAXST][2];   // rel-err partial sums per (stream segment, half-wave, iteration)\n", "    float red[SP_MAXSEG][2][SP_MAXST][2];\n    StepDiag sd;\n", 1),
     ("\n\n// Row stream of a workgroup.", "\n" + FN + "\n// Row stream of a workgroup.", 1),
     ("step_barrier();", "diag_barrier(sh);", _N_BARRIER),
-    ("        stream_pass<EXACT, ALPHA1, GEN>(a, sh, rm, a.n_tv, true, step, fresh);\n",
+    ("        stream_pass<EXACT, ALPHA1, GEN" + (", HALF>" if _SP == "HALF>" else ">") + "(a, sh, rm, a.n_tv, true, step, fresh);\n",
      "        {\n"
      "            unsigned long long* z = reinterpret_cast<unsigned long long*>(&sh.sd);\n"
      "            for (int i = threadIdx.x; i < (int)(sizeof(StepDiag) / 8); i += blockDim.x) z[i] = 0;\n"
      "            __syncthreads();\n"
      "        }\n"
-     "        stream_pass<EXACT, ALPHA1, GEN>(a, sh, rm, a.n_tv, true, step, fresh);\n"
+     "        stream_pass<EXACT, ALPHA1, GEN" + (", HALF>" if _SP == "HALF>" else ">") + "(a, sh, rm, a.n_tv, true, step, fresh);\n"
      "        __syncthreads();\n"
      "        if (g_sdiag && blockIdx.x < 64 && threadIdx.x == 0) {\n"
      "            unsigned long long* o = g_sdiag + (size_t)blockIdx.x * 64;\n"
