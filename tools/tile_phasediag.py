@@ -1,0 +1,86 @@
+"""Per-phase budget of one tv_tile_kernel launch (the strong-scaling kernel) from the diagnostic library built by
+`python3 tools/variant_build.py tdiag tools/patches/tile_phasediag.py` (exp_libs/lib_tdiag.so).
+Replays 20-step graph segments of the fused step at B chains of 3 x H x W and reads the stamps of the last two
+launches (100 MHz real-time counter, common to all CUs): per workgroup the kernel entry, loads issued + noise, loads
+landed + data term, inner iterations, rel-err / X side / u2 issued, arrival, and the last workgroup's finalisation.
+Prints the launch's critical path, the per-phase means over workgroups and the gap between two launches.
+Usage: PSGLA_LIB=exp_libs/lib_tdiag.so python3 tools/tile_phasediag.py [B] [H] [W]"""
+import ctypes
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("PSGLA_LIB", os.path.join(REPO, "exp_libs", "lib_tdiag.so"))
+sys.path.insert(0, REPO)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from psgla_for_posterior_sampling_amd import _native as N  # noqa: E402
+from psgla_for_posterior_sampling_amd import hip_ops as K  # noqa: E402
+from psgla_for_posterior_sampling_amd.engine import FusedTvChains  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+H = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+W = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+dev = torch.device("cuda:0")
+torch.manual_seed(0)
+xs = torch.rand((B, 3, H, W), device=dev)
+mask2d = (torch.rand((H, W), device=dev) > 0.5).to(torch.uint8)
+y = mask2d.float() * xs
+init = (mask2d.float() * y + (1 - mask2d.float()) * 0.5).contiguous()
+eng = FusedTvChains(init, y.contiguous(), mask2d, c1=1.5e-4, c2=0.055, sigma2=1.5e-5, alpha=1.0, ths=0.039,
+                    tv=K.TvConstants(n_it_max=10), seed=0, n_iter=4000, n_inter=10, n_inter_mmse=10,
+                    kernel_variant="tile")
+eng.run(200, graph_steps=20)                     # warm-up (graph captured)
+torch.cuda.synchronize()
+lib = N.lib()
+lib.psgla_tilediag_set_buffer.argtypes = [ctypes.c_void_p]
+lib.psgla_tilediag_set_buffer.restype = ctypes.c_int
+buf = torch.zeros((2, 4096, 8), dtype=torch.int64, device=dev)
+assert lib.psgla_tilediag_set_buffer(buf.data_ptr()) == 0
+ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+ev0.record()
+eng.run(20, graph_steps=20)
+ev1.record()
+torch.cuda.synchronize()
+lib.psgla_tilediag_set_buffer(None)
+ms = ev0.elapsed_time(ev1) / 20
+d = buf.cpu().numpy().astype(np.float64)
+G = int((d[0, :, 0] > 0).sum())
+assert G == int((d[1, :, 0] > 0).sum()) and G > 0, "both slots must hold one launch"
+later = 0 if d[0, :G, 0].min() > d[1, :G, 0].min() else 1
+A, Bq = d[1 - later, :G], d[later, :G]          # launch k - 1, launch k (10 ns ticks)
+us = lambda t: t / 100.0  # noqa: E731
+
+
+def budget(L):
+    t0 = L[:, 0].min()
+    last = int(np.argmax(L[:, 5]))
+    work = L[:, 1] > 0                          # workgroups that ran a tile (the rest only arrive)
+    ph = {
+        "dispatch_spread": us(L[:, 0].max() - t0),
+        "issue_noise": us((L[work, 1] - L[work, 0]).mean()),
+        "loads_data_term": us((L[work, 2] - L[work, 1]).mean()),
+        "iterations": us((L[work, 3] - L[work, 2]).mean()),
+        "relerr_x_u2_issue": us((L[work, 4] - L[work, 3]).mean()),
+        "store_drain_arrive": us((L[work, 5] - L[work, 4]).mean()),
+        "finalise": us(L[last, 6] - L[last, 5]),
+        "span": us(L[last, 6] - t0),
+        "last_wg_entry": us(L[last, 0] - t0),
+        "arrival_spread": us(L[:, 5].max() - L[:, 5].min()),
+    }
+    return ph, L[last, 6]
+
+
+pa, endA = budget(A)
+pb, _ = budget(Bq)
+gap = us(Bq[:, 0].min() - endA)
+out = {"B": B, "H": H, "W": W, "workgroups": G, "ms_per_step_events": round(ms, 5),
+       "launch_k": {k: round(v, 2) for k, v in pb.items()}, "launch_k-1": {k: round(v, 2) for k, v in pa.items()},
+       "gap_between_launches_us": round(gap, 2)}
+print(json.dumps(out))
+print(f"tile B={B} {H}x{W}: {G} workgroups, {ms * 1e3:.1f} us per step (events, diag build)")
+for k in pb:
+    print(f"  {k:>20s}: {pb[k]:7.2f} us   (previous launch {pa[k]:7.2f})")
+print(f"  {'gap to next launch':>20s}: {gap:7.2f} us")
