@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PSGLA_HIP_ABI_VERSION 9
+#define PSGLA_HIP_ABI_VERSION 10
 
 /* Max inner TV iterations the fused (temporally blocked) kernel handles. */
 #define PSGLA_TV_MAX_FUSED_IT 24
@@ -179,13 +179,15 @@ int psgla_tv_prox(const PsglaTvProx* d, void* stream);
 /* ---------------------------------------------------------------------------------
  * Generic (opaque-closure) building blocks.
  * ------------------------------------------------------------------------------- */
-/* out[b][e] = N(0,1) of "psgla noise v1" (seed, chain0+b, step, tag);  torch.randn at
- * restoration_algorithms.py:232 / :104 */
-int psgla_normal_fill(float* out, int32_t B, int64_t E, uint64_t seed, int32_t chain0,
+/* out[b][e] = N(0,1) of "psgla noise v2" (seed, chain0+b, step, tag);  torch.randn at
+ * restoration_algorithms.py:232 / :104.  A chain's E elements are rows of W (the image width:
+ * E = C*H*W); noise quads never straddle two rows (psgla_for_posterior_sampling_amd/csrc/noise.hpp).
+ * (ABI 10: W added; ABI <= 9 numbered the quads over the flat index, which differs for W % 4 != 0.) */
+int psgla_normal_fill(float* out, int32_t B, int64_t E, int32_t W, uint64_t seed, int32_t chain0,
                       const int64_t* d_step, int64_t step_offset, uint32_t tag, void* stream);
 
-/* Y = (X + c1*g) + c2*Z  (restoration_algorithms.py:232-236) */
-int psgla_langevin_update(const float* X, const float* g, float* Y, int32_t B, int64_t E, float c1,
+/* Y = (X + c1*g) + c2*Z  (restoration_algorithms.py:232-236); E = C*H*W elements per chain in rows of W */
+int psgla_langevin_update(const float* X, const float* g, float* Y, int32_t B, int64_t E, int32_t W, float c1,
                           float c2, uint64_t seed, int32_t chain0, const int64_t* d_step,
                           int64_t step_offset, void* stream);
 
@@ -200,8 +202,8 @@ int psgla_relax_accumulate(const float* Y, const float* D, float* X, float alpha
  *   X = (1-alpha)*Y + alpha*D  (X = D when alpha_is_one; Y may then be NULL);
  *   samples / block accumulators of step i (PsglaSchedule, as psgla_relax_accumulate);
  *   Y_next = (X + c1*g(X)) + c2*Z_{i+1},  g = ((-m)*(X - y))/sigma2,  Z_{i+1} the noise of step i+1;
- *   X is stored only when X != NULL.  Any H, W (H*W % 4 != 0: a scalar variant over the chain's
- *   element quads, same noise quads as psgla_langevin_update).  Identical to psgla_relax_accumulate +
+ *   X is stored only when X != NULL.  Any H, W (W % 4 != 0: a scalar variant over the chain's
+ *   row-aligned noise quads, as psgla_langevin_update).  Identical to psgla_relax_accumulate +
  *   psgla_inpaint_grad + psgla_langevin_update, in one pass (28 B/elem at alpha = 1). */
 int psgla_relax_langevin_inpaint(const float* Y, const float* D, float* X, float alpha, int32_t alpha_is_one,
                                  const float* y, int64_t y_chain_stride, const uint8_t* mask,
@@ -213,7 +215,7 @@ int psgla_relax_langevin_inpaint(const float* Y, const float* D, float* X, float
  *   proj = clip(X, c_min, c_max); X' = (X + delta*((gp - (X-proj)/lambd) + gd)) + brw*Z */
 int pnpula_update(const float* X, const float* gp, const float* gd, float* Xout, float delta,
                   float lambd, float brw, float c_min, float c_max, float* mean, float* sq,
-                  int32_t B, int64_t E, uint64_t seed, int32_t chain0, const PsglaSchedule* s,
+                  int32_t B, int64_t E, int32_t W, uint64_t seed, int32_t chain0, const PsglaSchedule* s,
                   void* stream);
 
 /* PnP-ULA step with the DNN prior fused ("V-ULA"): replaces, in one pass over the chain state,

@@ -11,13 +11,16 @@
  * are produced by the reference's own psgla/pnpula with torch.randn patched
  * to return this stream (tests/golden/make_golden.py).
  *
- * Stream definition ("psgla noise v1"), written independently of the HIP
+ * Stream definition ("psgla noise v2"), written independently of the HIP
  * implementation in psgla_for_posterior_sampling_amd/csrc/noise.hpp:
  *   ctr = {quad, step, tag, seed_hi}, key = {seed_lo, chain}
  *   x[0..3] = Philox4x32-10(ctr, key)   (Salmon et al., SC'11; Random123)
  *   (z0,z1) = BoxMuller(x0,x1), (z2,z3) = BoxMuller(x2,x3)
- *   element e of a chain's C*H*W image at Langevin step i takes z[e & 3]
- *   of quad e >> 2.
+ *   a chain's C*H*W image is C*H rows of W elements; element (row, col) at
+ *   Langevin step i takes z[col & 3] of quad row * ceil(W/4) + (col >> 2):
+ *   quads never straddle two rows.  For W % 4 == 0 that is z[e & 3] of quad
+ *   e >> 2 for the flat index e = row * W + col (the round-1..3 "v1" stream,
+ *   which numbered quads over the flat index for every W).
  *   BoxMuller(a,b): u = ((a>>8)+1)*2^-24 in (0,1];  r = sqrt(-2 log u);
  *     theta = 2*pi*(b>>8)*2^-24;  (r cos theta, r sin theta)
  *   log/sin/cos are fixed fp32 polynomials evaluated with explicit fmaf, and
@@ -134,16 +137,18 @@ void oracle_normal_quad(uint64_t seed, uint32_t chain, uint32_t step, uint32_t t
     box_muller(x[2], x[3], &z[2], &z[3]);
 }
 
-/* Fill n consecutive elements (element e -> quad e>>2, lane e&3) of one chain at one step. */
-void oracle_normal_fill(float *out, uint64_t n, uint64_t seed, uint32_t chain,
-                        uint32_t step, uint32_t tag) {
+/* Fill one chain's image of `rows` rows of W elements at one step (row-aligned quads, see above). */
+void oracle_normal_fill_rows(float *out, uint64_t rows, uint32_t W, uint64_t seed, uint32_t chain,
+                             uint32_t step, uint32_t tag) {
     float z[4];
-    uint64_t nq = (n + 3) >> 2;
-    for (uint64_t q = 0; q < nq; ++q) {
-        oracle_normal_quad(seed, chain, step, tag, (uint32_t)q, z);
-        for (int j = 0; j < 4; ++j) {
-            uint64_t e = (q << 2) + (uint64_t)j;
-            if (e < n) out[e] = z[j];
+    const uint64_t qw = ((uint64_t)W + 3) >> 2;        /* quads per row */
+    for (uint64_t r = 0; r < rows; ++r) {
+        for (uint64_t k = 0; k < qw; ++k) {
+            oracle_normal_quad(seed, chain, step, tag, (uint32_t)(r * qw + k), z);
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint64_t col = 4 * k + j;
+                if (col < W) out[r * W + col] = z[j];
+            }
         }
     }
 }

@@ -18,7 +18,7 @@ What it restates (all citations into /root/reference):
   tau=0.01, rho=1.99, sigma=1/(8 tau), tol=1e-5, warm start in x2/u2).  Its
   arithmetic is "parity unpinned" by any reference fixture.
 * the Gaussian noise ``torch.randn`` (restoration_algorithms.py:232, :104) is the
-  injected "psgla noise v1" stream from oracle/noise.c (see its header): the
+  injected "psgla noise v2" stream from oracle/noise.c (see its header): the
   golden fixtures were produced by the reference's own ``psgla``/``pnpula`` with
   ``torch.randn`` patched to return that stream (tests/golden/make_golden.py).
 
@@ -47,8 +47,8 @@ def _lib():
         if not os.path.exists(path):
             subprocess.run(["make", "-s", "-C", _HERE], check=True)
         lib = ctypes.CDLL(path)
-        lib.oracle_normal_fill.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
-                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+        lib.oracle_normal_fill_rows.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                                ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
         lib.oracle_philox4x32_10.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         lib.oracle_radius_table.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
         lib.oracle_angle_table.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
@@ -62,11 +62,14 @@ NOISE_TAG_LANGEVIN = 0
 
 def normal(shape, seed: int, chain: int, step: int, tag: int = NOISE_TAG_LANGEVIN) -> torch.Tensor:
     """One Langevin step's N(0,1) draw for one chain (replaces torch.randn at
-    restoration_algorithms.py:232 / :104).  Elements are numbered C-order over
-    ``shape`` (the chain's (1,C,H,W) image)."""
+    restoration_algorithms.py:232 / :104): "psgla noise v2" over ``shape`` (the
+    chain's (1,C,H,W) image) taken as rows of its last dimension -- element
+    (row, col) is output col & 3 of quad row * ceil(W/4) + col // 4 (oracle/noise.c)."""
     n = int(np.prod(shape))
+    W = int(shape[-1]) if len(shape) else 1
     out = np.empty(n, dtype=np.float32)
-    _lib().oracle_normal_fill(out.ctypes.data, n, seed & ((1 << 64) - 1), chain, step, tag)
+    if n:
+        _lib().oracle_normal_fill_rows(out.ctypes.data, n // W, W, seed & ((1 << 64) - 1), chain, step, tag)
     return torch.from_numpy(out).reshape(shape)
 
 

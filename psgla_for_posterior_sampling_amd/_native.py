@@ -11,7 +11,7 @@ import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PSGLA_LIB", os.path.join(_PKG, "libpsgla_hip.so"))
-ABI_VERSION = 9
+ABI_VERSION = 10
 TV_MAX_FUSED_IT = 24
 
 
@@ -66,8 +66,8 @@ _SIGNATURES = {
     "psgla_tv_step": (c_i32, [ctypes.POINTER(PsglaTvStep), ctypes.POINTER(PsglaSchedule), c_vp]),
     "psgla_tv_prox": (c_i32, [ctypes.POINTER(PsglaTvProx), c_vp]),
     "psgla_tv_step_kernel": (c_i32, [ctypes.POINTER(PsglaTvStep)]),
-    "psgla_normal_fill": (c_i32, [c_vp, c_i32, c_i64, c_u64, c_i32, c_vp, c_i64, c_u32, c_vp]),
-    "psgla_langevin_update": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i64, c_f, c_f, c_u64, c_i32, c_vp,
+    "psgla_normal_fill": (c_i32, [c_vp, c_i32, c_i64, c_i32, c_u64, c_i32, c_vp, c_i64, c_u32, c_vp]),
+    "psgla_langevin_update": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i64, c_i32, c_f, c_f, c_u64, c_i32, c_vp,
                                       c_i64, c_vp]),
     "psgla_relax_accumulate": (c_i32, [c_vp, c_vp, c_vp, c_f, c_i32, c_vp, c_vp, c_i32, c_i64,
                                        ctypes.POINTER(PsglaSchedule), c_vp]),
@@ -75,7 +75,7 @@ _SIGNATURES = {
                                              c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_f, c_f, c_f, c_u64, c_i32,
                                              ctypes.POINTER(PsglaSchedule), c_vp]),
     "pnpula_update": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_f, c_f, c_f, c_f, c_f, c_vp, c_vp, c_i32, c_i64,
-                              c_u64, c_i32, ctypes.POINTER(PsglaSchedule), c_vp]),
+                              c_i32, c_u64, c_i32, ctypes.POINTER(PsglaSchedule), c_vp]),
     "pnpula_prior_update": (c_i32, [c_vp, c_vp, c_f, c_f, c_vp, c_vp, c_i64, c_vp, c_i64, c_f, c_vp, c_f, c_f, c_f,
                                     c_f, c_f, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_u64, c_i32,
                                     ctypes.POINTER(PsglaSchedule), c_vp]),

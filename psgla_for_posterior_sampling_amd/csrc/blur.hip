@@ -238,15 +238,9 @@ __global__ void __launch_bounds__(BL_THREADS, (L <= 4 ? PSGLA_BLUR_WPE : 1)) blu
                 const size_t e0 = (size_t)tl.c * HW + (size_t)i * W + j;   // element index within the chain
                 const size_t o = (size_t)tl.b * a.C * HW + e0;
                 if (a.Y) {
-                    float z[4];
-                    if (vec) {
-                        normal_quad(a.seed, (uint32_t)(a.chain0 + tl.b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)(e0 >> 2), z);
-                    } else {
-#pragma unroll
-                        for (int kk = 0; kk < 4; ++kk)
-                            z[kk] = normal_elem(a.seed, (uint32_t)(a.chain0 + tl.b), (uint32_t)step, TAG_LANGEVIN,
-                                                (uint64_t)(e0 + kk));
-                    }
+                    float z[4];   // psgla noise v2: columns j .. j + 3 (j a multiple of 4) are one quad of the row
+                    normal_quad(a.seed, (uint32_t)(a.chain0 + tl.b), (uint32_t)step, TAG_LANGEVIN,
+                                noise_quad((size_t)tl.c * H + i, j, W), z);
                     // X of the tile from the staged copy (the same values as a.X)
                     const float* xr = &xb[(gp0 + m + 2 * L) * XS + gq + 2 * L];
                     float yo[4];
@@ -465,9 +459,9 @@ __global__ void __launch_bounds__(BL_THREADS, (L <= 4 ? 3 : 1)) blur_sep_kernel(
         const size_t e0 = (size_t)c * HW + (size_t)i * W + j;
         const size_t o = (size_t)b * a.C * HW + e0;
         if (a.Y) {
-            float z[4];
+            float z[4];   // psgla noise v2: columns j .. j + 3 (j a multiple of 4) are one quad of the row
+            normal_quad(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN, noise_quad((size_t)c * H + i, j, W), z);
             if (vec) {
-                normal_quad(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)(e0 >> 2), z);
                 const float4 xv = ld4(a.X + o);
                 *reinterpret_cast<float4*>(a.Y + o) =
                     make_float4((xv.x + a.c1 * gv[0]) + a.c2 * z[0], (xv.y + a.c1 * gv[1]) + a.c2 * z[1],
@@ -475,11 +469,7 @@ __global__ void __launch_bounds__(BL_THREADS, (L <= 4 ? 3 : 1)) blur_sep_kernel(
             } else {
 #pragma unroll
                 for (int kk = 0; kk < 4; ++kk) {
-                    if (j + kk < W) {
-                        const float zk = normal_elem(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN,
-                                                     (uint64_t)(e0 + kk));
-                        a.Y[o + kk] = (a.X[o + kk] + a.c1 * gv[kk]) + a.c2 * zk;
-                    }
+                    if (j + kk < W) a.Y[o + kk] = (a.X[o + kk] + a.c1 * gv[kk]) + a.c2 * z[kk];
                 }
             }
         } else if (vec) {

@@ -11,10 +11,25 @@ __device__ __forceinline__ long long read_step(const long long* d, long long off
     return (d ? *d : 0LL) + off;
 }
 
-__global__ void normal_fill_kernel(float* out, int B, long long E, unsigned long long seed, int chain0,
+// psgla noise v2 over a chain of E elements in rows of W (noise.hpp): quads never straddle two rows, so quad q
+// covers the chain's elements [e, e + n), e = (q / QW) W + 4 (q % QW), n = min(4, W - 4 (q % QW)), QW =
+// ceil(W / 4); (E / W) QW quads per chain.  W % 4 == 0: e = 4 q, n = 4 (no division).
+__device__ __forceinline__ long long quad_span(long long q, int W, int QW, int& n) {
+    if ((W & 3) == 0) {
+        n = 4;
+        return q << 2;
+    }
+    const long long row = q / QW;
+    const int k = (int)(q - row * QW);
+    n = min(4, W - 4 * k);
+    return row * W + 4 * k;
+}
+
+__global__ void normal_fill_kernel(float* out, int B, long long E, int W, unsigned long long seed, int chain0,
                                    const long long* d_step, long long off, uint32_t tag) {
     const long long step = read_step(d_step, off);
-    const long long Q = (E + 3) >> 2;
+    const int QW = (W + 3) >> 2;
+    const long long Q = (E / W) * QW;
     const long long total = (long long)B * Q;
     for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
          t += (long long)gridDim.x * blockDim.x) {
@@ -22,38 +37,39 @@ __global__ void normal_fill_kernel(float* out, int B, long long E, unsigned long
         const long long q = t - (long long)b * Q;
         float z[4];
         normal_quad(seed, (uint32_t)(chain0 + b), (uint32_t)step, tag, (uint32_t)q, z);
-        const long long e = q << 2;
+        int n;
+        const long long e = quad_span(q, W, QW, n);
         float* o = out + (size_t)b * E + e;
-        if (e + 3 < E && ((E & 3) == 0)) {
+        if ((W & 3) == 0) {
             *reinterpret_cast<float4*>(o) = make_float4(z[0], z[1], z[2], z[3]);
         } else {
-            for (int j = 0; j < 4; ++j)
-                if (e + j < E) o[j] = z[j];
+            for (int j = 0; j < n; ++j) o[j] = z[j];
         }
     }
 }
 
 // Y = (X + c1 g) + c2 Z   (restoration_algorithms.py:236)
-__global__ void langevin_update_kernel(const float* X, const float* g, float* Y, int B, long long E,
+__global__ void langevin_update_kernel(const float* X, const float* g, float* Y, int B, long long E, int W,
                                        float c1, float c2, unsigned long long seed, int chain0,
                                        const long long* d_step, long long off) {
-    // grid: (quads of a chain, chain); one noise quad = 4 consecutive elements of the chain
+    // grid: (noise quads of a chain, chain)
     const long long step = read_step(d_step, off);
-    const long long Q = (E + 3) >> 2;
+    const int QW = (W + 3) >> 2;
+    const long long Q = (E / W) * QW;
     const int b = blockIdx.y;
-    const bool vec = (E & 3) == 0;
+    const bool vec = (W & 3) == 0;
     for (long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x; q < Q;
          q += (long long)gridDim.x * blockDim.x) {
         float z[4];
         normal_quad(seed, (uint32_t)(chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)q, z);
-        const size_t i0 = (size_t)b * E + (size_t)(q << 2);
+        int n;
+        const size_t i0 = (size_t)b * E + (size_t)quad_span(q, W, QW, n);
         if (vec) {
             const float4 x = ld4(X + i0), gg = ld4(g + i0);
             st4(Y + i0, (x.x + c1 * gg.x) + c2 * z[0], (x.y + c1 * gg.y) + c2 * z[1],
                 (x.z + c1 * gg.z) + c2 * z[2], (x.w + c1 * gg.w) + c2 * z[3]);
         } else {
-            for (int j = 0; j < 4; ++j)
-                if ((q << 2) + j < E) Y[i0 + j] = (X[i0 + j] + c1 * g[i0 + j]) + c2 * z[j];
+            for (int j = 0; j < n; ++j) Y[i0 + j] = (X[i0 + j] + c1 * g[i0 + j]) + c2 * z[j];
         }
     }
 }
@@ -224,9 +240,8 @@ __global__ void relax_langevin_inpaint_kernel(const float* Y, const float* D, fl
     }
 }
 
-// The same pass for H*W % 4 != 0 (set1c / CBSD68 are 481 x 321): chain-linear quads, so the noise
-// quad of an element is the one psgla_langevin_update gives it (e >> 2 of the chain's C*H*W image);
-// scalar loads, one element at a time.  grid: (quads of a chain, chain)
+// The same pass for W % 4 != 0 (set1c / CBSD68 are 481 x 321): one thread per noise quad of the chain (row-aligned,
+// psgla noise v2), scalar loads.  grid: (noise quads of a chain, chain)
 __global__ void relax_langevin_inpaint_any_kernel(const float* Y, const float* D, float* X_out, float alpha,
                                                   int alpha1, const float* y, long long y_cs, const uint8_t* mask,
                                                   long long m_cs, float* Y_next, int B, int C, int H, int W,
@@ -239,19 +254,21 @@ __global__ void relax_langevin_inpaint_any_kernel(const float* Y, const float* D
     const int b = blockIdx.y;
     const float* yp = y + (size_t)b * y_cs;
     const uint8_t* mp = mask + (size_t)b * m_cs;
-    const long long Q = (E + 3) >> 2;
+    const int QW = (W + 3) >> 2;
+    const long long Q = (long long)C * H * QW;
     for (long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x; q < Q; q += (long long)gridDim.x * blockDim.x) {
         float z[4];
         normal_quad(seed, (uint32_t)(chain0 + b), (uint32_t)(step + 1), TAG_LANGEVIN, (uint32_t)q, z);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const long long e = 4 * q + j;
-            if (e >= E) break;
+        int n;
+        const long long e0 = quad_span(q, W, QW, n);
+        const long long m0 = e0 % HW;                      // a quad lies in one row, so in one plane
+        for (int j = 0; j < n; ++j) {
+            const long long e = e0 + j;
             const size_t idx = (size_t)b * E + e;
             const float x = alpha1 ? D[idx] : (1.0f - alpha) * Y[idx] + alpha * D[idx];
             if (X_out) X_out[idx] = x;
             acc_elem(s, step, idx, BE, x, mean, sq);
-            const float m = (float)mp[e % HW];
+            const float m = (float)mp[m0 + j];
             const float g = (-m * (x - yp[e])) / sigma2;
             Y_next[idx] = (x + c1 * g) + c2 * z[j];
         }
@@ -261,20 +278,22 @@ __global__ void relax_langevin_inpaint_any_kernel(const float* Y, const float* D
 // PnP-ULA (restoration_algorithms.py:104-115)
 __global__ void pnpula_update_kernel(const float* X, const float* gp, const float* gd, float* Xo,
                                      float delta, float lambd, float brw, float cmin, float cmax, int B,
-                                     long long E, float* mean, float* sq, unsigned long long seed,
+                                     long long E, int W, float* mean, float* sq, unsigned long long seed,
                                      int chain0, AccArgs s) {
-    // grid: (quads of a chain, chain)
+    // grid: (noise quads of a chain, chain)
     const long long step = read_step(s.d_step, s.off);
-    const long long Q = (E + 3) >> 2;
+    const int QW = (W + 3) >> 2;
+    const long long Q = (E / W) * QW;
     const size_t BE = (size_t)B * E;
     const int b = blockIdx.y;
-    const bool vec = (E & 3) == 0;
+    const bool vec = (W & 3) == 0;
     const AccStep st = acc_step(s, step, mean);
     for (long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x; q < Q;
          q += (long long)gridDim.x * blockDim.x) {
         float z[4];
         normal_quad(seed, (uint32_t)(chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)q, z);
-        const size_t i0 = (size_t)b * E + (size_t)(q << 2);
+        int n;
+        const size_t i0 = (size_t)b * E + (size_t)quad_span(q, W, QW, n);
         auto upd = [&](float x, float gpv, float gdv, float zz) {
             const float out = (x > cmin) ? x : cmin;
             const float proj = (out < cmax) ? out : cmax;
@@ -288,8 +307,7 @@ __global__ void pnpula_update_kernel(const float* X, const float* gp, const floa
             st4(Xo + i0, xn.x, xn.y, xn.z, xn.w);
             acc_quad(s, st, i0, BE, xn, mean, sq);
         } else {
-            for (int j = 0; j < 4; ++j) {
-                if ((q << 2) + j >= E) break;
+            for (int j = 0; j < n; ++j) {
                 const size_t i = i0 + j;
                 const float xn = upd(X[i], gp[i], gd[i], z[j]);
                 Xo[i] = xn;
@@ -305,17 +323,18 @@ __global__ void pnpula_update_kernel(const float* X, const float* gp, const floa
 // (deblurring: the stencil kernel's output), the projection, the update, the noise and the
 // accumulators in one pass -- read X, D, y, mean, sq (+ the shared mask), write X', mean, sq: 32 B/elem.
 // The same fp32 operations, in the same order, as DenoiserPrior's torch ops + psgla_inpaint_grad +
-// pnpula_update.  grid: (quads of a chain, chain); quads are chain-linear (the noise quads).
+// pnpula_update.  grid: (noise quads of a chain, chain): row-aligned quads (psgla noise v2).
 __global__ void pnpula_prior_update_kernel(const float* X, const float* D, float alpha, float s2, const float* gd,
                                            const float* y, long long y_cs, const uint8_t* mask, long long m_cs,
                                            float sigma2, float* Xo, float delta, float lambd, float brw, float cmin,
-                                           float cmax, int B, long long HW, long long E, float* mean, float* sq,
-                                           unsigned long long seed, int chain0, AccArgs s) {
+                                           float cmax, int B, long long HW, long long E, int W, float* mean,
+                                           float* sq, unsigned long long seed, int chain0, AccArgs s) {
     const long long step = read_step(s.d_step, s.off);
-    const long long Q = (E + 3) >> 2;
+    const int QW = (W + 3) >> 2;
+    const long long Q = (E / W) * QW;
     const size_t BE = (size_t)B * E;
     const int b = blockIdx.y;
-    const bool vec = (E & 3) == 0 && (HW & 3) == 0;
+    const bool vec = (W & 3) == 0;
     const AccStep st = acc_step(s, step, mean);
     const float* yp = y ? y + (size_t)b * y_cs : nullptr;
     const uint8_t* mp = mask ? mask + (size_t)b * m_cs : nullptr;
@@ -330,7 +349,9 @@ __global__ void pnpula_prior_update_kernel(const float* X, const float* D, float
          q += (long long)gridDim.x * blockDim.x) {
         float z[4];
         normal_quad(seed, (uint32_t)(chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)q, z);
-        const size_t i0 = (size_t)b * E + (size_t)(q << 2);
+        int n;
+        const long long e0 = quad_span(q, W, QW, n);
+        const size_t i0 = (size_t)b * E + (size_t)e0;
         if (vec) {
             const float4 x = ld4(X + i0), d = ld4(D + i0);
             float g[4];
@@ -338,7 +359,7 @@ __global__ void pnpula_prior_update_kernel(const float* X, const float* D, float
                 const float4 g4 = ld4(gd + i0);
                 g[0] = g4.x; g[1] = g4.y; g[2] = g4.z; g[3] = g4.w;
             } else {
-                const long long e = q << 2;
+                const long long e = e0;
                 const float4 yy = ld4(yp + e);
                 const uint32_t m = *reinterpret_cast<const uint32_t*>(mp + (e % HW));
                 g[0] = (-(float)(m & 0xFFu) * (x.x - yy.x)) / sigma2;
@@ -351,9 +372,8 @@ __global__ void pnpula_prior_update_kernel(const float* X, const float* D, float
             st4(Xo + i0, xn.x, xn.y, xn.z, xn.w);
             acc_quad(s, st, i0, BE, xn, mean, sq);
         } else {
-            for (int j = 0; j < 4; ++j) {
-                const long long e = (q << 2) + j;
-                if (e >= E) break;
+            for (int j = 0; j < n; ++j) {
+                const long long e = e0 + j;
                 const size_t i = i0 + j;
                 const float x = X[i];
                 const float gdv = gd ? gd[i] : (-(float)mp[e % HW] * (x - yp[e])) / sigma2;
@@ -437,24 +457,24 @@ using namespace psgla;
 
 extern "C" {
 
-int psgla_normal_fill(float* out, int32_t B, int64_t E, uint64_t seed, int32_t chain0, const int64_t* d_step,
+int psgla_normal_fill(float* out, int32_t B, int64_t E, int32_t W, uint64_t seed, int32_t chain0, const int64_t* d_step,
                       int64_t step_offset, uint32_t tag, void* stream) {
-    if (!out || B <= 0 || E <= 0) return fail(0, "psgla_normal_fill: bad arguments");
-    const long long total = (long long)B * ((E + 3) / 4);
+    if (!out || B <= 0 || E <= 0 || W <= 0 || E % W != 0) return fail(0, "psgla_normal_fill: bad arguments");
+    const long long total = (long long)B * (E / W) * ((W + 3) / 4);
     hipLaunchKernelGGL(normal_fill_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, out, B,
-                       (long long)E, (unsigned long long)seed, chain0, (const long long*)d_step,
+                       (long long)E, (int)W, (unsigned long long)seed, chain0, (const long long*)d_step,
                        (long long)step_offset, tag);
     return launch_check("normal_fill");
 }
 
-int psgla_langevin_update(const float* X, const float* g, float* Y, int32_t B, int64_t E, float c1, float c2,
-                          uint64_t seed, int32_t chain0, const int64_t* d_step, int64_t step_offset,
+int psgla_langevin_update(const float* X, const float* g, float* Y, int32_t B, int64_t E, int32_t W, float c1,
+                          float c2, uint64_t seed, int32_t chain0, const int64_t* d_step, int64_t step_offset,
                           void* stream) {
-    if (!X || !g || !Y || B <= 0 || E <= 0) return fail(0, "psgla_langevin_update: bad arguments");
-    const long long total = (long long)B * ((E + 3) / 4);
+    if (!X || !g || !Y || B <= 0 || E <= 0 || W <= 0 || E % W != 0) return fail(0, "psgla_langevin_update: bad arguments");
     if (B > 65535) return fail(0, "psgla_langevin_update: more than 65535 chains in one launch");
-    hipLaunchKernelGGL(langevin_update_kernel, dim3(grid_chain(E / 4 + 1, B), B), dim3(256), 0, (hipStream_t)stream, X,
-                       g, Y, B, (long long)E, c1, c2, (unsigned long long)seed, chain0,
+    const long long Q = (E / W) * ((W + 3) / 4);
+    hipLaunchKernelGGL(langevin_update_kernel, dim3(grid_chain(Q, B), B), dim3(256), 0, (hipStream_t)stream, X,
+                       g, Y, B, (long long)E, (int)W, c1, c2, (unsigned long long)seed, chain0,
                        (const long long*)d_step, (long long)step_offset);
     return launch_check("langevin_update");
 }
@@ -481,14 +501,15 @@ int psgla_relax_accumulate(const float* Y, const float* D, float* X, float alpha
 }
 
 int pnpula_update(const float* X, const float* gp, const float* gd, float* Xout, float delta, float lambd,
-                  float brw, float c_min, float c_max, float* mean, float* sq, int32_t B, int64_t E,
+                  float brw, float c_min, float c_max, float* mean, float* sq, int32_t B, int64_t E, int32_t W,
                   uint64_t seed, int32_t chain0, const PsglaSchedule* s, void* stream) {
-    if (!X || !gp || !gd || !Xout || !s || B <= 0 || E <= 0) return fail(0, "pnpula_update: bad arguments");
+    if (!X || !gp || !gd || !Xout || !s || B <= 0 || E <= 0 || W <= 0 || E % W != 0)
+        return fail(0, "pnpula_update: bad arguments");
     if (s->n_inter_mmse >= 0 && (!mean || !sq || !s->acc_coef)) return fail(0, "pnpula_update: accumulators missing");
-    const long long total = (long long)B * ((E + 3) / 4);
     if (B > 65535) return fail(0, "pnpula_update: more than 65535 chains in one launch");
-    hipLaunchKernelGGL(pnpula_update_kernel, dim3(grid_chain(E / 4 + 1, B), B), dim3(256), 0, (hipStream_t)stream, X, gp,
-                       gd, Xout, delta, lambd, brw, c_min, c_max, B, (long long)E, mean, sq,
+    const long long Q = (E / W) * ((W + 3) / 4);
+    hipLaunchKernelGGL(pnpula_update_kernel, dim3(grid_chain(Q, B), B), dim3(256), 0, (hipStream_t)stream, X, gp,
+                       gd, Xout, delta, lambd, brw, c_min, c_max, B, (long long)E, (int)W, mean, sq,
                        (unsigned long long)seed, chain0, make_acc(s));
     return launch_check("pnpula_update");
 }
@@ -503,9 +524,10 @@ int pnpula_prior_update(const float* X, const float* D, float alpha, float s2, c
     if (s->n_inter_mmse >= 0 && (!mean || !sq || !s->acc_coef)) return fail(0, "pnpula_prior_update: accumulators missing");
     if (B > 65535) return fail(0, "pnpula_prior_update: more than 65535 chains in one launch");
     const long long HW = (long long)H * W, E = (long long)C * HW;
-    hipLaunchKernelGGL(pnpula_prior_update_kernel, dim3(grid_chain(E / 4 + 1, B), B), dim3(256), 0, (hipStream_t)stream,
+    const long long Q = (long long)C * H * ((W + 3) / 4);
+    hipLaunchKernelGGL(pnpula_prior_update_kernel, dim3(grid_chain(Q, B), B), dim3(256), 0, (hipStream_t)stream,
                        X, D, alpha, s2, gd, y, (long long)y_chain_stride, mask, (long long)mask_chain_stride, sigma2,
-                       Xout, delta, lambd, brw, c_min, c_max, B, HW, E, mean, sq, (unsigned long long)seed, chain0,
+                       Xout, delta, lambd, brw, c_min, c_max, B, HW, E, (int)W, mean, sq, (unsigned long long)seed, chain0,
                        make_acc(s));
     return launch_check("pnpula_prior_update");
 }
@@ -533,14 +555,14 @@ int psgla_relax_langevin_inpaint(const float* Y, const float* D, float* X, float
     if (s->n_inter_mmse >= 0 && (!mean || !sq || !s->acc_coef))
         return fail(0, "psgla_relax_langevin_inpaint: accumulators missing");
     if ((long long)B * C > 65535) return fail(0, "psgla_relax_langevin_inpaint: more than 65535 planes in one launch");
-    if (((long long)H * W) % 4 == 0)
+    if (W % 4 == 0)   // the vector pass's plane-linear quads are the noise quads only for W % 4 == 0
         hipLaunchKernelGGL(relax_langevin_inpaint_kernel, dim3(grid_chain((long long)H * W / 4 + 1, B * C), B * C),
                            dim3(256), 0, (hipStream_t)stream, Y, D, X, alpha, (int)(alpha_is_one != 0), y,
                            (long long)y_chain_stride, mask, (long long)mask_chain_stride, Y_next, B, C, H, W, sigma2,
                            c1, c2, (unsigned long long)seed, chain0, mean, sq, make_acc(s));
     else
         hipLaunchKernelGGL(relax_langevin_inpaint_any_kernel,
-                           dim3(grid_chain(((long long)C * H * W + 3) / 4, B), B), dim3(256), 0, (hipStream_t)stream,
+                           dim3(grid_chain((long long)C * H * ((W + 3) / 4), B), B), dim3(256), 0, (hipStream_t)stream,
                            Y, D, X, alpha, (int)(alpha_is_one != 0), y, (long long)y_chain_stride, mask,
                            (long long)mask_chain_stride, Y_next, B, C, H, W, sigma2, c1, c2,
                            (unsigned long long)seed, chain0, mean, sq, make_acc(s));

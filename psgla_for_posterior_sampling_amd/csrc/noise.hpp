@@ -1,11 +1,16 @@
 // In-register Gaussian noise for the Langevin step (replaces torch.randn at
 // /root/reference/restoration_algorithms.py:232 (psgla) and :104 (pnpula)).
 //
-// "psgla noise v1": counter-based, so any element of any chain at any step can be
+// "psgla noise v2": counter-based, so any element of any chain at any step can be
 // regenerated anywhere (tiles recompute their halo's noise instead of reading it):
 //   ctr = {quad, step, tag, seed_hi}, key = {seed_lo, chain}
 //   Philox4x32-10 -> 4 x u32 -> two Box-Muller pairs -> 4 x N(0,1) fp32
-//   element e of a chain's C*H*W image uses output (e & 3) of quad (e >> 2).
+//   a chain's C*H*W image is C*H rows of W elements; element (row, col) uses output
+//   (col & 3) of quad row * ceil(W/4) + (col >> 2): a quad never straddles two rows, so
+//   a lane holding 4 columns of a row (from a multiple of 4) needs exactly one Philox for
+//   any W.  For W % 4 == 0 this is quad e >> 2, output e & 3 of the flat index e (the
+//   "v1" stream of rounds 1-3, which numbered quads over the flat index for every W and
+//   made W % 4 != 0 rows straddle two quads).
 // log / sin / cos are fixed fp32 polynomials evaluated with explicit fmaf and the
 // square root is IEEE-rounded (sqrtf under the default -fhip-fp32-correctly-rounded-divide-sqrt;
 // NB: HIP's __fsqrt_rn is the native approximation), so the stream is bit-identical to the
@@ -105,13 +110,9 @@ __device__ __forceinline__ void normal_quad(uint64_t seed, uint32_t chain, uint3
     box_muller(c2, c3, z[2], z[3]);
 }
 
-// one element (generic, unaligned paths)
-__device__ __forceinline__ float normal_elem(uint64_t seed, uint32_t chain, uint32_t step, uint32_t tag,
-                                             uint64_t e) {
-    float z[4];
-    normal_quad(seed, chain, step, tag, (uint32_t)(e >> 2), z);
-    const uint32_t j = (uint32_t)(e & 3u);
-    return j == 0 ? z[0] : (j == 1 ? z[1] : (j == 2 ? z[2] : z[3]));
+// the quad holding element (row, col) of a chain's image of W-element rows
+__device__ __forceinline__ uint32_t noise_quad(size_t row, int col, int W) {
+    return (uint32_t)(row * (size_t)((W + 3) >> 2) + (size_t)(col >> 2));
 }
 
 }  // namespace psgla

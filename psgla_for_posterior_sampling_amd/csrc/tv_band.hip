@@ -72,6 +72,9 @@ __device__ __forceinline__ void tv_tile(const TvArgs& a, int plane, int tile, in
             float Yv[CPL], xs[CPL], us0[CPL], us1[CPL];
             if (FRONT == FRONT_INPAINT) {
                 float X[CPL], yo[CPL], mk[CPL], Z[CPL];
+                // psgla noise v2: the lane's 4 columns (gj0 a multiple of 4) are one quad of the row
+                normal_quad(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN,
+                            noise_quad((size_t)c * H + gi[r], gj0, W), Z);
                 const float* xin = a.x[par_in];
                 const float* yb = a.yobs + (size_t)b * a.y_cs + (size_t)c * HW + (size_t)gi[r] * W + gj0;
                 const uint8_t* mb = a.mask + (size_t)b * a.m_cs + (size_t)gi[r] * W + gj0;
@@ -82,9 +85,6 @@ __device__ __forceinline__ void tv_tile(const TvArgs& a, int plane, int tile, in
                     X[0] = xv.x; X[1] = xv.y; X[2] = xv.z; X[3] = xv.w;
                     yo[0] = yy.x; yo[1] = yy.y; yo[2] = yy.z; yo[3] = yy.w;
                     mk[0] = (float)mm.x; mk[1] = (float)mm.y; mk[2] = (float)mm.z; mk[3] = (float)mm.w;
-                    const size_t e = ((size_t)c * H + gi[r]) * W + gj0;
-                    normal_quad(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN,
-                                (uint32_t)(e >> 2), Z);
                 } else {
 #pragma unroll
                     for (int k = 0; k < CPL; ++k) {
@@ -92,10 +92,7 @@ __device__ __forceinline__ void tv_tile(const TvArgs& a, int plane, int tile, in
                         X[k] = ok ? xin[base + k] : 0.f;
                         yo[k] = ok ? yb[k] : 0.f;
                         mk[k] = ok ? (float)mb[k] : 0.f;
-                        const size_t e = ((size_t)c * H + gi[r]) * W + gj0 + k;
-                        Z[k] = ok ? normal_elem(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step,
-                                                TAG_LANGEVIN, e)
-                                  : 0.f;
+                        Z[k] = ok ? Z[k] : 0.f;
                     }
                 }
 #pragma unroll

@@ -177,7 +177,7 @@ struct RowGeo {
     size_t pbase;       // element offset of the (real) plane in the (B, C, H, ldw) state buffers
     size_t ybase;       // element offset of the plane in the observation (chain stride y_cs)
     size_t mbase;       // byte offset of the chain's mask (chain stride m_cs)
-    size_t ebase;       // unpadded element index of the plane's first element in its chain (noise counter)
+    size_t rbase;       // the plane's first row among its chain's C*H rows (noise counter, psgla noise v2)
     int bb;             // chain (batch entry)
     int f0;             // first column of the wave window (GEN; 0 otherwise)
     int cc0, cc1;       // core columns of the segment
@@ -197,7 +197,7 @@ __device__ __forceinline__ RowGeo row_geo(const TvArgs& a, int vp) {
     g.pbase = (size_t)sg.rp * HW;
     g.ybase = (size_t)g.bb * a.y_cs + (size_t)cc * HW;
     g.mbase = (size_t)g.bb * a.m_cs;
-    g.ebase = (size_t)cc * a.H * a.W;
+    g.rbase = (size_t)cc * a.H;
     g.f0 = sg.f0;
     g.cc0 = sg.cc0;
     g.cc1 = sg.cc1;
@@ -501,7 +501,7 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamSharedT<A1>& s
 // (front / stage / back roles, one barrier per step).  Inlined at two call sites: the main
 // pass and the rare early-stop recompute, each with its own register allocation.
 // GEN: the row pitch is not the image width (rows padded: W % 4 != 0) -- the last-column, norm
-// and noise-window handling of such rows, compiled only into the kernels that need it
+// handling of such rows, compiled only into the kernels that need it
 template <bool EXACT, bool ALPHA1, bool GEN, bool HALF>
 __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA1>& sh, const RowMap& rm, const int n,
                                             const bool track, const long long step, const bool fresh) {
@@ -543,9 +543,6 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
         const int fw = w;                                  // front wave id (stream rows q % 4 == fw)
         uint32_t ph0 = 0, ph1 = 0, ph2 = 0, ph3 = 0;
         float zn0 = 0.f, zn1 = 0.f, zn2 = 0.f, zn3 = 0.f;
-        uint32_t pq0 = 0, pq1 = 0, pq2 = 0, pq3 = 0;          // second quad (W % 4 != 0 rows)
-        float zq0 = 0.f, zq1 = 0.f, zq2 = 0.f, zq3 = 0.f;
-        int esh = 0;
         int gjf = gj0;                                      // first column of the lane in row q (GEN:
         bool okf = lane_ok;                                 // per column segment)
         const float* xin = a.x[par_in];
@@ -597,40 +594,21 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
                     gjf = g.f0 + CPL * lc;
                     okf = g.on && gjf < W;
                 }
-                // element index in the chain's unpadded C*H*W image: the noise stream
-                // does not depend on the row pitch
-                const size_t e = g.ebase + (size_t)rc_cur.r * W + gjf;
-                esh = (int)(e & 3);                         // the same for every lane of the row
-                uint32_t c0 = (uint32_t)(e >> 2), c1 = (uint32_t)step, c2 = TAG_LANGEVIN,
-                         c3 = (uint32_t)(a.seed >> 32);
+                // psgla noise v2: the lane's 4 columns (gjf a multiple of 4) are one quad of the row, for
+                // any W and independent of the row pitch
+                uint32_t c0 = noise_quad(g.rbase + (size_t)rc_cur.r, gjf, W), c1 = (uint32_t)step,
+                         c2 = TAG_LANGEVIN, c3 = (uint32_t)(a.seed >> 32);
                 philox4x32_10(c0, c1, c2, c3, (uint32_t)a.seed, (uint32_t)(a.chain0 + g.bb));
                 ph0 = c0; ph1 = c1; ph2 = c2; ph3 = c3;
-                if (GEN && esh != 0) {                     // the lane's 4 elements span two quads
-                    uint32_t d0 = (uint32_t)(e >> 2) + 1u, d1 = (uint32_t)step, d2 = TAG_LANGEVIN,
-                             d3 = (uint32_t)(a.seed >> 32);
-                    philox4x32_10(d0, d1, d2, d3, (uint32_t)a.seed, (uint32_t)(a.chain0 + g.bb));
-                    pq0 = d0; pq1 = d1; pq2 = d2; pq3 = d3;
-                }
             }
             step_barrier();
             // ---- phase 1: Box-Muller pair 1; DMA part 1
             front_issue(1, q + 4, rc_dma);
             box_muller(ph0, ph1, zn0, zn1);
-            if (GEN && esh != 0) box_muller(pq0, pq1, zq0, zq1);
             step_barrier();
             // ---- phase 2: Box-Muller pair 2; DMA part 2
             front_issue(2, q + 4, rc_dma);
             box_muller(ph2, ph3, zn2, zn3);
-            if (GEN && esh != 0) {
-                box_muller(pq2, pq3, zq2, zq3);
-                // element i of the lane = output (esh + i) of the two-quad window
-                const float w8[8] = {zn0, zn1, zn2, zn3, zq0, zq1, zq2, zq3};
-                float r4[CPL];
-#pragma unroll
-                for (int i = 0; i < CPL; ++i)
-                    r4[i] = esh == 1 ? w8[i + 1] : (esh == 2 ? w8[i + 2] : w8[i + 3]);
-                zn0 = r4[0]; zn1 = r4[1]; zn2 = r4[2]; zn3 = r4[3];
-            }
             step_barrier();
             // ---- phase 3: data term of row q -> ring 0 / Y ring; DMA part 3 of row q + 4
             {

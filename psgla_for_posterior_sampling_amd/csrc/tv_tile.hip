@@ -105,20 +105,10 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
     float Zn[R][CPL];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        // element index in the chain's unpadded C*H*W image: the noise does not depend on the row pitch
-        const size_t e = ((size_t)c * H + (rv[r] ? gi[r] : 0)) * W + gj0;
-        normal_quad(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)(e >> 2), Zn[r]);
-        if (GEN) {
-            const int esh = (int)(e & 3);               // the same for every lane of the row
-            if (esh != 0) {                             // the lane's 4 elements span two quads
-                float zq[CPL];
-                normal_quad(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN, (uint32_t)(e >> 2) + 1u, zq);
-                const float w8[8] = {Zn[r][0], Zn[r][1], Zn[r][2], Zn[r][3], zq[0], zq[1], zq[2], zq[3]};
-#pragma unroll
-                for (int i = 0; i < CPL; ++i)
-                    Zn[r][i] = esh == 1 ? w8[i + 1] : (esh == 2 ? w8[i + 2] : w8[i + 3]);
-            }
-        }
+        // psgla noise v2: the lane's 4 columns (from a multiple of 4) are one quad of the row, for any W and
+        // independent of the row pitch
+        normal_quad(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN,
+                    noise_quad((size_t)c * H + (rv[r] ? gi[r] : 0), gj0, W), Zn[r]);
     }
     // ---- 3. data term Y = (X + c1 g) + c2 Z, TV start state
 #pragma unroll

@@ -39,6 +39,11 @@ def _bce(x: torch.Tensor):
     return B, x.numel() // B
 
 
+def _row(x: torch.Tensor) -> int:
+    """Row length of a chain's image for the noise (psgla noise v2: quads never straddle two rows)."""
+    return int(x.shape[-1])
+
+
 # ------------------------------------------------------------------------------------
 # accumulation schedule (restoration_algorithms.py:240-271)
 # ------------------------------------------------------------------------------------
@@ -100,7 +105,7 @@ class Schedule:
 def normal_fill(out: torch.Tensor, seed: int, chain0: int, step: int, tag: int = NOISE_TAG_LANGEVIN,
                 d_step: torch.Tensor | None = None):
     B, E = _bce(out)
-    N.check(N.lib().psgla_normal_fill(_ptr(out, name="out"), B, E, seed & (2 ** 64 - 1), chain0,
+    N.check(N.lib().psgla_normal_fill(_ptr(out, name="out"), B, E, _row(out), seed & (2 ** 64 - 1), chain0,
                                       d_step.data_ptr() if d_step is not None else None, step, tag,
                                       _stream()), "psgla_normal_fill")
     return out
@@ -112,7 +117,7 @@ def langevin_update(X, g, c1: float, c2: float, seed: int, chain0: int, step: in
         out = torch.empty_like(X)
     B, E = _bce(X)
     N.check(N.lib().psgla_langevin_update(_ptr(X, name="X"), _ptr(g, name="g"), _ptr(out, name="Y"), B, E,
-                                          c1, c2, seed & (2 ** 64 - 1), chain0,
+                                          _row(X), c1, c2, seed & (2 ** 64 - 1), chain0,
                                           d_step.data_ptr() if d_step is not None else None, step,
                                           _stream()), "psgla_langevin_update")
     return out
@@ -153,7 +158,7 @@ def pnpula_update(X, gp, gd, X_out, delta: float, lambd: float, brw: float, c_mi
     s = sched.struct(use_device_step, step)
     N.check(N.lib().pnpula_update(_ptr(X, name="X"), _ptr(gp, name="gp"), _ptr(gd, name="gd"),
                                   _ptr(X_out, name="Xout"), delta, lambd, brw, c_min, c_max,
-                                  _ptr(mean, name="mean"), _ptr(sq, name="sq"), B, E, seed & (2 ** 64 - 1),
+                                  _ptr(mean, name="mean"), _ptr(sq, name="sq"), B, E, _row(X), seed & (2 ** 64 - 1),
                                   chain0, ctypes.byref(s), _stream()), "pnpula_update")
     return X_out
 

@@ -19,7 +19,7 @@ Dispatch:
   kernels; a ``BlurFidelity`` data term is fused with the Langevin update (one stencil kernel).
 ``pnpula`` with a :class:`~denoisers.DenoiserPrior` prior and a typed data term runs
 :class:`engine.UlaChains` (hipGraph-replayed steps: config 5).
-The Gaussian noise is the in-kernel "psgla noise v1" stream of (seed, chain) instead of
+The Gaussian noise is the in-kernel "psgla noise v2" stream of (seed, chain) instead of
 torch's generator (whose CUDA stream depends on the device's CU count); extra keyword
 ``chain0`` gives the global id of the first chain when a batch is sharded over GPUs.
 

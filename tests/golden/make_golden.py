@@ -9,7 +9,8 @@ What is executed from the reference (read-only, never copied into the repo):
   imported as a module with the two unused module-level imports stubbed
   (``cv2`` :8 and ``deepinv.optim.data_fidelity.L2`` :9; neither is installed
   and neither is used by psgla/pnpula).  ``torch.randn`` inside that module is
-  redirected to the "psgla noise v1" stream (oracle/noise.c), so the reference
+  redirected to the psgla noise stream (oracle/noise.c; every fixture has W % 4 == 0,
+  where the round-1 "v1" and the current "v2" numbering are one stream), so the reference
   consumes exactly the noise the HIP kernels generate.
 * the data-fidelity set-up of sampling_images.py:283-341 and the parameter
   derivation of sampling_images.py:100-123 / :147-198, executed from the

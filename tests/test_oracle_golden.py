@@ -180,3 +180,20 @@ def test_params_fixture_matches_survey_table():
     assert tv["N"] == 1000 and tv["n_inter"] == 10 and tv["lambd"] == 10.0
     assert abs(tv["delta_float"] / tv["lambd"] / tv["sigma2t"] - 10.0) < 1e-4
     assert p["pnp_ula_DRUNet_N1e6"]["n_inter"] == 1000
+
+
+def test_noise_v2_row_aligned_quads():
+    """psgla noise v2 (oracle/noise.c): a chain's image is rows of W; element (row, col) takes output col & 3 of
+    quad row * ceil(W/4) + col // 4, so a row's noise does not depend on W beyond its quad count -- an odd-width
+    image equals the first W columns of the image padded to a multiple of 4 -- and W % 4 == 0 is the flat
+    numbering (quad e // 4, output e % 4) of rounds 1-3 that the golden fixtures were made with."""
+    for (c, h, w) in ((3, 5, 7), (1, 4, 5), (2, 3, 321), (1, 2, 1)):
+        wq = (w + 3) // 4 * 4
+        a = orc.normal((1, c, h, w), 11, 3, 17)
+        b = orc.normal((1, c, h, wq), 11, 3, 17)
+        assert torch.equal(a, b[..., :w])
+    # row 1 of a 5-wide image starts a new quad (quad 2), unlike the flat numbering (element 5 = quad 1, output 1)
+    z = orc.normal((1, 1, 2, 5), 0, 0, 0).flatten()
+    q = orc.normal((1, 1, 1, 12), 0, 0, 0).flatten()       # quads 0, 1, 2 of the same stream
+    assert torch.equal(z[5:9], q[8:12])
+    assert torch.equal(z[:4], q[:4]) and z[4] == q[4]

@@ -19,8 +19,11 @@ from psgla_for_posterior_sampling_amd.fidelity import inpainting_problem  # noqa
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+TRANSPOSE = len(sys.argv) > 3 and sys.argv[3] == "T"     # the other orientation (3 x 321 x 481: W = 481)
 dev = torch.device("cuda:0")
 im = np.float32(SI.read_image(os.path.join(REPO, "tests", "golden", "set1c", "castle.png")) / 255.)
+if TRANSPOSE:
+    im = np.ascontiguousarray(np.transpose(im, (1, 0, 2)))
 im_t = torch.from_numpy(np.transpose(im, (2, 0, 1))).float().unsqueeze(0).to(dev)
 dg, y, init, mask2d, _ = inpainting_problem(im_t, seed_ip=0)
 s, lam = 10 / 255.0, 10.0
@@ -38,7 +41,15 @@ dt = time.perf_counter() - t0
 Xl, Ml, M2l = eng.lists()
 rec, _ = metrics.analyse_run(im, [x[0] if B > 1 else x for x in Xl[-3:]], [m[0] if B > 1 else m for m in Ml],
                              [m[0] if B > 1 else m for m in M2l], y, init)
-print(json.dumps({"workload": "psgla+TV inpainting, set1c castle 3x481x321", "chains": B, "n_iter": N,
+Hc, Wc = im.shape[0], im.shape[1]
+# roofline fraction of the fused step: compulsory bytes per launch (bench.algorithmic_bytes_per_launch, this run's
+# schedule) / the per-step time / 8 TB/s
+sys.path.insert(0, REPO)
+from bench import algorithmic_bytes_per_launch  # noqa: E402
+nb = algorithmic_bytes_per_launch(B, 3, Hc, Wc, 100, N - 100, max(1, N // 1000), max(1, N // 1000))
+frac = nb / (dt / (N - 100)) / 8e12
+print(json.dumps({"workload": f"psgla+TV inpainting, set1c castle 3x{Hc}x{Wc}", "chains": B, "n_iter": N,
                   "kernel": eng.main_kernel, "ms_per_step": round(dt / (N - 100) * 1e3, 5),
                   "image_steps_per_s": round(B * (N - 100) / dt, 1), "PSNR_MMSE": round(rec["PSNR_MMSE"], 3),
-                  "PSNR_y": round(rec["PSNR_y"], 3), "blocks": len(Ml)}))
+                  "PSNR_y": round(rec["PSNR_y"], 3), "blocks": len(Ml),
+                  "algorithmic_bytes_per_step": round(nb), "roofline_frac": round(frac, 4)}))
