@@ -27,7 +27,7 @@ template <int R, int NW>
 struct TileShared {
     float4 zrow[NW][WAVE];             // first-row z of each wave (read by the wave above)
     float4 urow[NW][WAVE];             // last-row u2[..., 0] of each wave (read by the wave below)
-    float4 mst[tile_mst_rows(NW, R)][2][WAVE];   // mean / sq of the tile's core rows (LDS-DMA at the start)
+    float4 mst[tile_mst_rows(NW, R)][2][WAVE];   // mean / sq of the tile's core rows (LDS-DMA after the data term)
     float2 red[MAXIT][NW][4];          // rel_err partial sums per (iteration, wave, 16-lane row of the wave)
     int s_stop[MAXG];
     int s_flag, s_item, s_next;
@@ -69,7 +69,7 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
     float z[R][CPL], yv[R][CPL];
     int gi[R];
     bool rv[R], core[R];
-    // ---- 1. every load of the tile in flight: state and observation to registers, mean / sq by DMA
+    // ---- 1. every load the first iteration needs in flight: state, observation and mask to registers
     float4 fX[R], fY[R], fU0[R], fU1[R], fXS[R];
     uint32_t fM[R];
 #pragma unroll
@@ -89,16 +89,6 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
             }
             fY[r] = ld4(a.yobs + (size_t)b * a.y_cs + (size_t)c * HW + (size_t)gi[r] * L + gj0);
             fM[r] = *reinterpret_cast<const uint32_t*>(a.mask + (size_t)b * a.m_cs + (size_t)gi[r] * L + gj0);
-        }
-    }
-    if (need_prev && n_it >= 0) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (rv[r] && core[r]) {
-                const size_t base = poff + (size_t)gi[r] * L + gjc;
-                glds16(a.mean[par_in] + base, &sh.mst[gi[r] - r0][0][0]);
-                glds16(a.sq[par_in] + base, &sh.mst[gi[r] - r0][1][0]);
-            }
         }
     }
     // ---- 2. the noise of the tile's rows (no memory dependence: overlaps the loads)
@@ -140,6 +130,20 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
     }
     sh.urow[w][lane] = make_float4(u0[R - 1][0], u0[R - 1][1], u0[R - 1][2], u0[R - 1][3]);
     __syncthreads();
+    // The previous mean / sq of the core rows, LDS-DMA'd only now (round 4): the accumulator update after the last
+    // iteration is their only reader, so these 8 B per element land during the iterations instead of competing
+    // with the loads above, which the first iteration waits for.  The iteration barriers drain LDS only
+    // (lgkmcnt), so nothing waits for this DMA before store_x_side's vmcnt(0).
+    if (need_prev && n_it >= 0) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (rv[r] && core[r]) {
+                const size_t base = poff + (size_t)gi[r] * L + gjc;
+                glds16(a.mean[par_in] + base, &sh.mst[gi[r] - r0][0][0]);
+                glds16(a.sq[par_in] + base, &sh.mst[gi[r] - r0][1][0]);
+            }
+        }
+    }
 
     // ---- 4. inner TV iterations (deepinv 0.2.1 TVDenoiser, the stream kernel's arithmetic)
     const bool lastlane = gj0 + CPL == W;              // holds column W-1: no forward difference there

@@ -56,8 +56,11 @@ us = lambda t: t / 100.0  # noqa: E731
 
 def budget(L):
     t0 = L[:, 0].min()
-    last = int(np.argmax(L[:, 5]))
     work = L[:, 1] > 0                          # workgroups that ran a tile (the rest only arrive)
+    # the finalising workgroup: its stamp 6 lies in this launch (a stale 6 of another launch is older than t0)
+    fin = np.where(L[:, 6] >= L[:, 5].max() - 1)[0] if (L[:, 6] >= t0).any() else np.array([], dtype=int)
+    fin = int(fin[np.argmax(L[fin, 6])]) if fin.size else int(np.argmax(L[:, 5]))
+    end = max(L[fin, 6], L[:, 5].max())
     ph = {
         "dispatch_spread": us(L[:, 0].max() - t0),
         "issue_noise": us((L[work, 1] - L[work, 0]).mean()),
@@ -65,12 +68,12 @@ def budget(L):
         "iterations": us((L[work, 3] - L[work, 2]).mean()),
         "relerr_x_u2_issue": us((L[work, 4] - L[work, 3]).mean()),
         "store_drain_arrive": us((L[work, 5] - L[work, 4]).mean()),
-        "finalise": us(L[last, 6] - L[last, 5]),
-        "span": us(L[last, 6] - t0),
-        "last_wg_entry": us(L[last, 0] - t0),
+        "finalise": us(L[fin, 6] - L[fin, 5]),
+        "span": us(end - t0),
         "arrival_spread": us(L[:, 5].max() - L[:, 5].min()),
+        "mean_workgroup_span": us((L[work, 5] - L[work, 0]).mean()),
     }
-    return ph, L[last, 6]
+    return ph, end
 
 
 pa, endA = budget(A)
