@@ -132,10 +132,10 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
             const int grid = ((P * s.nbands * s.st_nsegs + 7) / 8) * 8;   // tile_kernel: 8 runs of tiles
             // (the two-phase arrival counter keeps a count of workgroups in 15 bits)
             if (grid > 32767) return fail(0, "psgla_tv_step: more than 32767 tiles in one launch");
-            // several copies of the rel-err sums only where many tiles share a chain (castle at B = 1: 246 tiles,
-            // 34.8 -> 33.0 us); with 15-66 tiles per chain the last workgroup's reads of 8 copies cost more
-            // (+4-5 %) than the queueing they save (profiles/r03s_tile_norm_copies_ab.txt)
-            if (s.norm_copies < 1 || s.C * s.nbands * s.st_nsegs < 128) s.norm_copies = 1;
+            // several copies of the rel-err sums only where many tiles share a chain: with the finaliser's copy
+            // reads issued back to back (round 4), 8 copies cost 8 chains of 30 tiles +1.6 % and save castle at
+            // batch 2 (108 tiles per chain) 3.5 % and at batch 1 (246) 5 % (profiles/r04k_tile_fin_ab.txt)
+            if (s.norm_copies < 1 || s.C * s.nbands * s.st_nsegs < 64) s.norm_copies = 1;
             const bool gen = !(s.ldw == s.W && s.st_nsegs == 1);
             if (launch_tile(s, dim3(grid), st, EXACT, ALPHA1, gen)) return launch_check("tv_tile_kernel");
             return fail(0, "psgla_tv_step: internal error: no tile kernel of this shape");

@@ -308,6 +308,9 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
     if (n_it > 0) iteration(n_it - 1, std::true_type{});
     // ---- 5. rel_err partial sums -> the chain's norms (one fp64 atomic per iteration and workgroup)
     if (track) {
+        // (on wave 0, before the u2 stores: spreading the sums over waves delays every wave's u2 stores -- 8
+        // chains +4.3 %, castle at batch 1 +9 % -- and moving them after the u2 stores gains nothing:
+        // profiles/r04l_tile_ab.txt, r04m_tile_ab.txt)
         const int t = threadIdx.x;
         if (t >= trk_lo(a) && t <= trk_hi(a) && t < n_it) {
             double sd = 0.0, sn = 0.0;
@@ -422,15 +425,35 @@ __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
     for (int i = threadIdx.x; i < G * MAXIT; i += blockDim.x) {
         const int g = i / MAXIT, t = i - g * MAXIT;
         if (t >= trk_lo(a) && t <= trk_hi(a) && t < a.n_tv) {
-            // read by agent-scope atomics (+0.0, returning), as they were written: 8-B agent atomics on both
-            // sides of the hand-off, performed where the producers' adds were
+            // read by agent-scope atomics (exchange with 0.0: read and reset in one operation), as they were
+            // written: 8-B agent atomics on both sides of the hand-off, performed where the producers' adds were
+            // With several copies, the first 8 copies' reads are issued back to back and waited for once (round 4:
+            // one round trip instead of one per copy: castle at batch 1 -4.8 %, profiles/r04k_tile_fin_ab.txt),
+            // then added in copy order as before; one copy keeps the plain pair of reads
+            const size_t cstride = (size_t)a.B * a.n_tv * 2;
+            double* const n0 = a.norms + ((size_t)g * a.n_tv + t) * 2;
             double nd = 0.0, nn = 0.0;
-            for (int cp = 0; cp < a.norm_copies; ++cp) {   // the copies in a fixed order
-                double* const nc = a.norms + (size_t)cp * ((size_t)a.B * a.n_tv * 2);
-                nd += __hip_atomic_fetch_add(&nc[((size_t)g * a.n_tv + t) * 2], 0.0, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-                nn += __hip_atomic_fetch_add(&nc[((size_t)g * a.n_tv + t) * 2 + 1], 0.0, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
+            if (a.norm_copies == 1) {
+                nd += __hip_atomic_exchange(n0, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                nn += __hip_atomic_exchange(n0 + 1, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                double vd[8], vn[8];
+#pragma unroll
+                for (int cp = 0; cp < 8; ++cp) {
+                    vd[cp] = vn[cp] = 0.0;
+                    if (cp < a.norm_copies) {
+                        vd[cp] = __hip_atomic_exchange(n0 + cp * cstride, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        vn[cp] = __hip_atomic_exchange(n0 + cp * cstride + 1, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+#pragma unroll
+                for (int cp = 0; cp < 8; ++cp) {
+                    if (cp < a.norm_copies) { nd += vd[cp]; nn += vn[cp]; }
+                }
+                for (int cp = 8; cp < a.norm_copies; ++cp) {   // beyond 8 copies (not used by the engine): in order
+                    nd += __hip_atomic_exchange(n0 + cp * cstride, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    nn += __hip_atomic_exchange(n0 + cp * cstride + 1, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
             const float rel = (float)sqrt(nd) / (float)sqrt(nn);
             if (rel < a.tol) atomicOr(&sh.s_stop[g], 1 << t);
@@ -474,7 +497,8 @@ __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < a.B * a.n_tv * 2 * a.norm_copies; i += blockDim.x) a.norms[i] = 0.0;
+    // (the norm copies were zeroed by the exchanges that read them; entries outside the tracked iterations are
+    // never written)
     if (threadIdx.x == 0) {
         // both counts out (the other workgroups' phase-2 adds may still be landing: an add, not a store); the
         // counter is 0 once the kernel has completed
