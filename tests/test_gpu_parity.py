@@ -912,13 +912,15 @@ def test_tile_kernel_equals_stream_kernel_real_shapes(B, H, W):
 
 
 @pytest.mark.parametrize("B,H,W,tol", [(8, 256, 256, 3e-3), (8, 256, 256, 1e-3), (16, 256, 256, 3e-3),
-                                       (1, 481, 321, 3e-3), (2, 321, 481, 3e-3)])
+                                       (1, 481, 321, 3e-3), (2, 321, 481, 3e-3), (1, 256, 256, 3e-3),
+                                       (2, 256, 256, 3e-3)])
 def test_tile_kernel_early_stop_handoff_full_size(B, H, W, tol):
     """The tile kernel's fence-free step hand-off (sc1 stores, rel-err sums as agent atomics read back by
     the last workgroup's agent atomics) under a tolerance at which deepinv's early stop fires: 40 steps of
-    8 chains (48-row tiles) or 16 chains (72-row tiles) at 3 x 256 x 256, and the reference's real shapes at
-    the CLI's batch sizes (castle 481 x 321 at B = 1, 321 x 481 at B = 2: >= 128 tiles per chain, so the
-    rel-err sums are spread over the workspace's 8 norm copies, ABI 8), bit-identical to the row-streaming
+    8 chains (48-row tiles) or 16 chains (72-row tiles) at 3 x 256 x 256, the reference's real shapes at
+    the CLI's batch sizes (castle 481 x 321 at B = 1, 321 x 481 at B = 2) and 256 x 256 at B = 1, 2 (32-row
+    tiles): >= 64 tiles per chain, so the rel-err sums are spread over the workspace's 8 norm copies (ABI 8;
+    read back to back and reset by exchange since round 4), bit-identical to the row-streaming
     kernel (which keeps its release / acquire fences and one norm copy), and different from the same run
     without early stops (so stops did fire).  After every run the whole norms workspace (all copies) is
     zero again: the finaliser summed and cleared every copy."""
