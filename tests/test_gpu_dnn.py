@@ -115,12 +115,13 @@ def test_denoiser_chains_vs_oracle():
     assert rel(M, Mr) < REL_TOL_MEAN
 
 
-@pytest.mark.parametrize("H,W,deblur", [(32, 48, False), (37, 45, False), (32, 48, True)])
+@pytest.mark.parametrize("H,W,deblur", [(32, 48, False), (37, 45, False), (36, 45, False), (32, 48, True)])
 def test_ula_chains_graph_equals_step_loop(H, W, deblur):
     """pnpula with a DenoiserPrior (DRUNet/DnCNN prior of sampling_images.py:156-157): UlaChains
     (hipGraph replay, the prior's arithmetic + data term + update fused in one V-ULA pass,
     pnpula_prior_update) == the step-by-step loop with the prior as an opaque closure (DenoiserPrior's
-    torch ops, the data-term kernel, pnpula_update), bit for bit: inpainting on 4-aligned and odd planes,
+    torch ops, the data-term kernel, pnpula_update), bit for bit: inpainting on 4-aligned and odd planes
+    (36 x 45: H*W % 4 == 0 with W % 4 != 0, the row-quad noise of psgla noise v2),
     deblurring (the stencil's gd fed to the fused pass)."""
     from psgla_for_posterior_sampling_amd import restoration_algorithms as RA
     from psgla_for_posterior_sampling_amd.denoisers import DenoiserPrior
@@ -206,11 +207,13 @@ def test_dncnn_fused_epilogue_equals_torch_layers():
 
 
 @pytest.mark.parametrize("alpha", [1.0, 0.6])
-def test_relax_langevin_inpaint_odd_plane_equals_unfused(alpha):
-    """H*W % 4 != 0 (set1c / CBSD68 are 481 x 321): the chain-quad variant of the fused pass equals
-    relax_accumulate + inpaint_grad + langevin_update bit for bit."""
+@pytest.mark.parametrize("H,W", [(37, 45), (36, 45)])
+def test_relax_langevin_inpaint_odd_plane_equals_unfused(alpha, H, W):
+    """W % 4 != 0 (set1c / CBSD68 are 481 x 321): the row-quad variant of the fused pass equals
+    relax_accumulate + inpaint_grad + langevin_update bit for bit -- also where H*W % 4 == 0 but W % 4 != 0
+    (36 x 45), which the vector pass's plane-linear quads must not take (psgla noise v2 quads follow the rows)."""
     from psgla_for_posterior_sampling_amd import hip_ops as K
-    B, C, H, W = 2, 3, 37, 45
+    B, C = 2, 3
     dg, _ = problem(B=B, H=H, W=W)
     g = torch.Generator(device=DEV).manual_seed(6)
     c1, c2, seed = 0.8 * (1 / 255.0) ** 2, 0.011, 9
