@@ -100,3 +100,15 @@ def test_kernel_dispatch_rules_on_the_host():
     assert k == -1 and "kernel_variant" in err
     k, err = kind(1, 481, 321, ldw=324, variant=1)               # the band kernel needs ldw == W
     assert k == -1 and "row pitch" in err
+
+
+def test_ctypes_arity_matches_header():
+    """Every entry point's parameter count in include/psgla_hip.h equals the ctypes binding's (an ABI change that
+    adds a parameter -- ABI 10's image width W of the noise entry points -- must reach both)."""
+    from psgla_for_posterior_sampling_amd import _native as N
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    for name, (_res, args) in N._SIGNATURES.items():
+        m = re.search(r"\b" + re.escape(name) + r"\s*\(([^)]*)\)\s*;", src)
+        assert m, name
+        params = [p for p in m.group(1).split(",") if p.strip() and p.strip() != "void"]
+        assert len(params) == len(args), f"{name}: header {len(params)} vs ctypes {len(args)}"
