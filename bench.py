@@ -284,6 +284,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     live_kern_ms = ev0.elapsed_time(ev1) / steps     # kernel + its launch boundary, in the timed region
+    eng.check_handoff()                              # the tile kernel's early-stop guard (after the timed region)
     if world > 1:
         import torch.distributed as dist
         t = torch.tensor([dt], device=dev if backend == "nccl" else "cpu")

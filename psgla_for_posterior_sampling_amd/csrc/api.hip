@@ -188,6 +188,8 @@ static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
         { g_sel_err = "psgla_tv_step: shape not supported by the streaming kernel"; return -1; }
     if (d->kernel_variant < 0 || d->kernel_variant > 4 || d->kernel_variant == 3)
         { g_sel_err = "psgla_tv_step: kernel_variant must be 0 (auto), 1 (band), 2 (stream) or 4 (tile)"; return -1; }
+    if (d->stream_windows < 0 || d->stream_windows > 2)
+        { g_sel_err = "psgla_tv_step: stream_windows must be 0, 1 or 2"; return -1; }
     // small-batch tile kernel: forced (variant 4) or, in auto mode, when all tiles fit in one round
     // on the CUs (a row stream would be mostly pipeline fill: strong scaling's 64/N chains per GPU)
     a.tile_r = 0;

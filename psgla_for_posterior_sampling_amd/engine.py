@@ -39,7 +39,7 @@ class FusedTvChains:
         self.shape = (B, C, H, Wd)
         self.W = Wd
         # rows padded to a multiple of 4 columns so that every width runs on the streaming kernel
-        # (psgla_kernels.hip: ldw); the padding columns are scratch and every result is a view
+        # (csrc/tv_stream.hip, tv_tile.hip: ldw); the padding columns are scratch and every result is a view
         # of the first W columns
         if kernel_variant not in KERNEL_VARIANTS:
             raise ValueError(f"kernel_variant must be one of {sorted(KERNEL_VARIANTS)}")

@@ -378,7 +378,8 @@ def main(argv=None):
             record, mask, name = gathered[i]
             write_result(pars, os.path.join(path_result, "im_" + str(i)), name, record, mask)
             records.append(record)
-        if n_img:
+        # not in the reference's output: only for the runs it has no counterpart of (batched or sharded)
+        if n_img and (world > 1 or getattr(pars, "batch_size", 1) > 1):
             print("Dataset ({} images): mean output PSNR {:.2f} dB / mean output SSIM {:.2f}".format(
                 n_img, psnr_sum / n_img, ssim_sum / n_img))
     if world > 1:

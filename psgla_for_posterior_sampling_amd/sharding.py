@@ -102,6 +102,8 @@ def gather_records(local: dict, world: int, rank: int, device, obj_group=None):
             arrays["__mask__"] = ("torch", mask.detach().cpu().numpy())
         layout = {}
         for k, (kind, a) in arrays.items():
+            if a.dtype.kind in "iub" and a.size and int(np.abs(a.astype(np.int64)).max()) >= 2 ** 53:
+                raise ValueError(f"gather_records: integer array {k!r} has values beyond 2**53 (float64 transport)")
             flat = np.ascontiguousarray(a, dtype=np.float64).reshape(-1)
             layout[k] = (kind, str(a.dtype), tuple(a.shape), off, flat.size)
             chunks.append(flat)
