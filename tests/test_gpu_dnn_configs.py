@@ -180,7 +180,7 @@ def test_dnn_config_64_chains_full_size_properties(workload):
     from psgla_for_posterior_sampling_amd import restoration_algorithms as RA
     from psgla_for_posterior_sampling_amd.denoisers import DenoiserPrior
     from psgla_for_posterior_sampling_amd.fidelity import deblurring_problem, inpainting_problem
-    B, H, W, n, nm = 64, 256, 256, 9, 2
+    B, H, W, n, nm = 64, 256, 256, 12, 2
     g = torch.Generator(device=DEV).manual_seed(21)
     x = torch.rand((1, 3, H, W), generator=g, device=DEV)
     if workload == "dncnn-deblur":
