@@ -1,8 +1,9 @@
 #!/bin/bash
 # Interleaved A/B of libraries within ONE GPU call: for each repetition, every library in turn runs bench.py
-# with the same arguments (no CPU leg).  "prod" = the product library; NAME = exp_libs/lib_NAME.so.
+# with the same arguments (no CPU leg).  "prod" = the product library; NAME = exp_libs/lib_NAME.so; VAR=VALUE = the
+# product library with that environment variable set (e.g. PSGLA_STREAM_LAYOUT=2).
 # stdout/stderr of every leg are kept (gpurun_out/ab_TAG/<lib>_<rep>.{json,err}); a failing leg ends the script
-# with its stderr printed.  One line per leg: tag | lib | rep | ms_per_step | kernel_ms | kernel.
+# with its stderr printed.  One line per leg: tag | lib | rep | ms_per_step | kernel_ms | iso kernel_ms_isolated | kernel.
 # Usage: tools/ab_bench.sh TAG REPS "BENCH ARGS" lib1 lib2 ...
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -11,7 +12,7 @@ O=gpurun_out/ab_$T
 mkdir -p $O
 for rep in $(seq 1 $REPS); do
   for v in "$@"; do
-    if [ "$v" = "prod" ]; then LIBENV=""; else LIBENV="PSGLA_LIB=exp_libs/lib_$v.so"; fi
+    if [ "$v" = "prod" ]; then LIBENV=""; elif [[ "$v" == *=* ]]; then LIBENV="$v"; else LIBENV="PSGLA_LIB=exp_libs/lib_$v.so"; fi
     env $LIBENV timeout -k 10 180 python3 bench.py --no-cpu $ARGS > $O/${v}_$rep.json 2> $O/${v}_$rep.err
     rc=$?
     if [ $rc -ne 0 ]; then echo "leg $v rep $rep failed rc=$rc"; tail -20 $O/${v}_$rep.err; exit $rc; fi
@@ -19,7 +20,7 @@ for rep in $(seq 1 $REPS); do
 import json, sys
 t, v, rep, path = sys.argv[1:]
 d = json.loads(open(path).read().strip().splitlines()[-1])
-print(f"{t} | {v:>10s} | {rep} | {d['ms_per_step']:.5f} | {d['roofline']['kernel_ms']:.5f} | {d['roofline']['kernel']}", flush=True)
+print(f"{t} | {v:>22s} | {rep} | {d['ms_per_step']:.5f} | {d['roofline']['kernel_ms']:.5f} | iso {d['roofline']['kernel_ms_isolated']:.5f} | {d['roofline']['kernel']}", flush=True)
 PY
   done
 done
