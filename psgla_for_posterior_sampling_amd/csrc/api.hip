@@ -250,12 +250,6 @@ static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
         a.st_halo = d->n_tv;
         a.st_nsegs = stream_segments(a.W, a.ldw, d->n_tv, &a.st_seg_w);
         a.st_half = 0;
-        // row-stream layout: classic (16 waves, one inner iteration per stage wave) or merged (12 waves, two
-        // iterations on the first n_tv - 6 stage waves); PSGLA_STREAM_LAYOUT=1 / 2 forces one (diagnostics)
-        {
-            static const int env_layout = [] { const char* e = getenv("PSGLA_STREAM_LAYOUT"); return e ? atoi(e) : 0; }();
-            a.st_merged = env_layout == 2 ? 1 : 0;
-        }
         a.st_nvp = d->B * d->C * a.st_nsegs;
         // half windows when they leave fewer lanes idle (castle-like 481 x 321: 2 windows of 256 columns hold
         // 321 -- 63 % of the lanes; 3 half-windows of 128 -- 84 %); stream_windows 1 keeps whole windows

@@ -127,7 +127,6 @@ struct TvArgs {
                                     // half-wave; 256 < W <= 324 at n_tv = 10: a third of the lanes fewer idle)
     int st_nvp;                     // stream kernel virtual planes: (plane, segment) items, or pairs of them (st_half)
     int fin_inline;                 // stream kernel: 1 = the last workgroup finalises the step
-    int st_merged;                  // stream kernel: 1 = merged layout (12 waves, two inner iterations per stage wave)
     int tile_r;                     // > 0: small-batch tile kernel with tile_r rows per wave (one tile per workgroup)
     int tile_nw;                    // tile kernel: waves per workgroup (16 or 8)
     int norm_copies;                // tile kernel: copies of norms its rel-err sums are spread over (>= 1)
@@ -211,8 +210,6 @@ constexpr int SP_FRONT = 4;
 constexpr int SP_BACK = 2;
 constexpr int SP_MAXST = 10;
 constexpr int SP_YRING = 32;
-constexpr int SP_MRG_STW = 6;     // merged layout: stage waves (n_tv - 6 of them run two inner iterations)
-constexpr int SP_MRG_THREADS = (SP_FRONT + SP_MRG_STW + SP_BACK) * 64;   // 12 waves
 constexpr int SP_MAXSEG = 4;      // planes touched by one workgroup's row stream (split mode)
 constexpr int SP_NOSEG = 1 << 30; // "no further segment start"
 

@@ -497,198 +497,12 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamSharedT<A1>& s
     flush();
 }
 
-// ---------------------------------------------------------------------------------------
-// Stage wave of the merged layout (MRG): KI (1 or 2) consecutive inner iterations k0 .. k0 + KI - 1 on one wave.
-// Iteration i's lookahead row is j - 2 i (j: iteration 0's).  At each step the wave
-//   1. issues the LDS reads of its input row j (ring k0 - 1, or the front's staging for FIRST),
-//   2. runs the dual update of every iteration's row j - 2 i - 2 (inputs in registers); iteration i's output
-//      row (x2^k, u2^k) IS iteration i + 1's lookahead row j - 2 (i + 1): it goes straight into that
-//      iteration's primal, no LDS ring between them; the last iteration's output goes to its ring,
-//   3. runs the primal updates (iteration 0's once its reads have landed).
-// Two iterations per wave halve the ring writes / reads of those iterations (the one lever the round-3
-// ablation singles out: no ring traffic at all = -17 %) and shorten the pipeline (lag 5 per wave of two
-// iterations instead of 3 + 3).  Every iteration keeps its own row triple, segment walk and rel-err sums.
-// TRKM: bit i = iteration i tracks deepinv's rel-err (iterations 3 .. n - 1, 1-based).
-// ---------------------------------------------------------------------------------------
-struct ItState {
-    int k;              // inner iteration (1-based)
-    int Qk;             // rows the iteration runs (bottom-halo trim)
-    int sacc, nb;       // segment of the primal row, next segment start
-    bool fprev;         // the previous primal row started a segment
-    int lastk, nreal;   // GEN: of the primal row's column segment
-    bool core;
-    float lsd, lsn;     // rel-err partial sums of segment sacc
-};
-template <int I> using IC = std::integral_constant<int, I>;
-
-template <bool EXACT, bool GEN, bool A1, bool FIRST, bool HALF, int KI, int TRKM>
-__device__ __forceinline__ void stage_loop_m(const TvArgs& a, StreamSharedT<A1>& sh, const RowMap& rm, int k0, int n,
-                                             int nsteps, int tbeg, int lane, int lastk0, int nreal0, bool core0,
-                                             bool fresh) {
-    StageRow R[KI][3];
-    ItState S[KI];
-    const float zero[CPL] = {0.f, 0.f, 0.f, 0.f};
-    const int Qb = rm.Q - rm.hbot;
-    const int qc0 = rm.htop, qc1 = Qb;            // core stream rows
-    int jn = 0;                                   // lookahead steps of the wave
-#pragma unroll
-    for (int i = 0; i < KI; ++i) {
-        S[i].k = k0 + i;
-        S[i].Qk = min(rm.Q, Qb + n - S[i].k + 1);
-        S[i].sacc = 0;
-        S[i].nb = next_seg_start(rm, 0);
-        S[i].fprev = false;
-        S[i].lastk = lastk0; S[i].nreal = nreal0; S[i].core = core0;
-        S[i].lsd = 0.f; S[i].lsn = 0.f;
-        jn = max(jn, S[i].Qk + 2 * i + 2);
-    }
-    const int rin = StreamSharedT<A1>::rk(k0 - 1), rout = StreamSharedT<A1>::rk(k0 + KI - 1);
-    auto set_geo = [&](auto Ic) {
-        constexpr int I = decltype(Ic)::value;
-        if (GEN) {
-            const SegGeo g = seg_geo<GEN, HALF>(a, rm.pl(S[I].sacc), lane >> 5);
-            const int gj = g.f0 + CPL * lcol<HALF>(lane);
-            S[I].lastk = a.W - 1 - gj;
-            S[I].nreal = min(CPL, max(0, a.W - gj));
-            S[I].core = g.on && gj < a.W && gj >= g.cc0 && gj < g.cc1;
-        }
-    };
-    auto flush = [&](auto Ic) {
-        constexpr int I = decltype(Ic)::value;
-        if constexpr (((TRKM >> I) & 1) != 0) {
-            ItState& s = S[I];
-            const int kk = s.k - 1;
-            if (HALF) {
-                const float2 rs = row_sum2(s.core ? s.lsd : 0.f, s.core ? s.lsn : 0.f);
-                const int xi = __float_as_int(rs.x), yi = __float_as_int(rs.y);
-                float d0 = __int_as_float(__builtin_amdgcn_readlane(xi, 0)) + __int_as_float(__builtin_amdgcn_readlane(xi, 16));
-                float d1 = __int_as_float(__builtin_amdgcn_readlane(xi, 32)) + __int_as_float(__builtin_amdgcn_readlane(xi, 48));
-                const float q0 = __int_as_float(__builtin_amdgcn_readlane(yi, 0)) + __int_as_float(__builtin_amdgcn_readlane(yi, 16));
-                const float q1 = __int_as_float(__builtin_amdgcn_readlane(yi, 32)) + __int_as_float(__builtin_amdgcn_readlane(yi, 48));
-                if (!EXACT) { d0 *= a.rho * a.rho; d1 *= a.rho * a.rho; }
-                if (lane == 0) {
-                    sh.red[s.sacc][0][kk][0] = d0; sh.red[s.sacc][0][kk][1] = q0;
-                    sh.red[s.sacc][1][kk][0] = d1; sh.red[s.sacc][1][kk][1] = q1;
-                }
-            } else {
-                float d = wave_sum(s.core ? s.lsd : 0.f);
-                const float q = wave_sum(s.core ? s.lsn : 0.f);
-                if (!EXACT) d *= a.rho * a.rho;
-                if (lane == 0) { sh.red[s.sacc][0][kk][0] = d; sh.red[s.sacc][0][kk][1] = q; }
-            }
-            s.lsd = 0.f; s.lsn = 0.f;
-        }
-    };
-    // iteration 0's input row j: ring k0 - 1, or (FIRST) the front's staging of row j (x2 = X, u2; a TV
-    // restart: x2 = Y, u2 = 0, by selects)
-    auto load_row = [&](int j, float4& X2, float4& U0, float4& U1, float4& YY) {
-        float4 A, B;
-        YY = sh.y[j & (SP_YRING - 1)][lane];
-        if (FIRST) {
-            const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 sX = sh.stX(j & 3, j)[lane];
-            const float4 sA = sh.stUa(j & 3, j)[lane];
-            const float4 sB = sh.stUb(j & 3, j)[lane];
-            X2 = sel4(fresh, YY, sX);
-            A = sel4(fresh, zero4, sA);
-            B = sel4(fresh, zero4, sB);
-        } else {
-            const int sl = j & 1;
-            X2 = sh.x2[rin][sl][lane];
-            A = sh.ua[rin][sl][lane];
-            B = sh.ub[rin][sl][lane];
-        }
-        U0 = make_float4(A.x, A.z, B.x, B.z);
-        U1 = make_float4(A.y, A.w, B.y, B.w);
-    };
-    auto store_row = [&](int i, const StageRow& r, const float (&un0)[CPL], const float (&un1)[CPL]) {
-        const int so = i & 1;
-        sh.x2[rout][so][lane] = make_float4(r.x2n[0], r.x2n[1], r.x2n[2], r.x2n[3]);
-        sh.ua[rout][so][lane] = make_float4(un0[0], un1[0], un0[1], un1[1]);
-        sh.ub[rout][so][lane] = make_float4(un0[2], un1[2], un0[3], un1[3]);
-    };
-    float4 X2[KI], U0[KI], U1[KI], YY[KI];
-    // The updates run unconditionally on every step (register flow without branches, so each iteration keeps
-    // only its two live rows across a step); only their effects -- ring stores, rel-err sums, segment walk --
-    // are guarded by the row's validity.  Rows outside 0 .. Qk - 1 (pipeline fill / drain) compute on stale
-    // registers and are never stored: a valid row never reads them (row 0 and segment starts take u0 = 0 above,
-    // the last row's dual no z below, iteration I + 1's valid rows come from iteration I's valid rows).
-    // dual of iteration I's row d = j - 2 I - 2 (slot (d mod 3) of its triple); its output feeds iteration I + 1
-    auto dual = [&](auto Ic, auto PHc, int j) {
-        constexpr int I = decltype(Ic)::value, PH = decltype(PHc)::value;
-        constexpr int s2 = ((PH - 2 * I - 2) % 3 + 6) % 3, s1 = (s2 + 1) % 3;
-        ItState& s = S[I];
-        const int d = j - 2 * I - 2;
-        const StageRow& p2 = R[I][s2];
-        float un0[CPL], un1[CPL];
-        if (d + 1 < s.Qk && !s.fprev) stage_phase_b<EXACT, true, GEN>(a, p2, R[I][s1].z, GEN ? p2.lk : s.lastk, un0, un1);
-        else stage_phase_b<EXACT, false, GEN>(a, p2, zero, GEN ? p2.lk : s.lastk, un0, un1);
-        if constexpr (I + 1 < KI) {
-            X2[I + 1] = make_float4(p2.x2n[0], p2.x2n[1], p2.x2n[2], p2.x2n[3]);
-            U0[I + 1] = make_float4(un0[0], un0[1], un0[2], un0[3]);
-            U1[I + 1] = make_float4(un1[0], un1[1], un1[2], un1[3]);
-            YY[I + 1] = sh.y[d & (SP_YRING - 1)][lane];
-        } else {
-            if (d >= 0 && d < s.Qk) store_row(d, p2, un0, un1);
-        }
-    };
-    // primal of iteration I's lookahead row ji = j - 2 I (slot ji mod 3); the row above is slot (ji - 1) mod 3
-    auto primal = [&](auto Ic, auto PHc, int j) {
-        constexpr int I = decltype(Ic)::value, PH = decltype(PHc)::value;
-        constexpr int sc = ((PH - 2 * I) % 3 + 6) % 3, sp = (sc + 2) % 3;
-        constexpr bool TRK = ((TRKM >> I) & 1) != 0;
-        ItState& s = S[I];
-        const int ji = j - 2 * I;
-        StageRow& cur = R[I][sc];
-        float rd = 0.f, rn = 0.f;
-        const bool fj = ji == s.nb && ji < s.Qk;
-        if (fj) {                   // row ji starts a new segment (split mode only)
-            flush(Ic);
-            ++s.sacc;
-            s.nb = next_seg_start(rm, ji);
-            set_geo(Ic);
-        }
-        // the first row of the stream or of a segment has no row above: u0 = 0 there (selects: two inlined
-        // copies of the update get merged by the compiler into one behind a pointer select, in scratch)
-        const bool top = fj || ji == 0;
-        float pu0[CPL];
-#pragma unroll
-        for (int kk = 0; kk < CPL; ++kk) pu0[kk] = top ? 0.f : R[I][sp].u0[kk];
-        stage_phase_a<EXACT, TRK, GEN, HALF>(a, X2[I], U0[I], U1[I], YY[I], pu0, cur, rd, rn, s.nreal);
-        if (GEN) cur.lk = s.lastk;
-        if (TRK && ji >= qc0 && ji < qc1) { s.lsd += rd; s.lsn += rn; }
-        if (ji >= 0 && ji < s.Qk) s.fprev = fj;
-    };
-    auto step = [&](auto PHc, int j) {
-        load_row(j, X2[0], U0[0], U1[0], YY[0]);
-        dual(IC<0>{}, PHc, j);
-        if constexpr (KI > 1) dual(IC<1>{}, PHc, j);
-        if constexpr (KI > 1) primal(IC<1>{}, PHc, j);
-        primal(IC<0>{}, PHc, j);
-        step_barrier();
-    };
-    int t = 0;
-    for (; t < tbeg; ++t) step_barrier();
-    int j = 0;
-    for (; j + 2 < jn; j += 3) {
-        step(IC<0>{}, j);
-        step(IC<1>{}, j + 1);
-        step(IC<2>{}, j + 2);
-    }
-    if (j < jn) step(IC<0>{}, j);
-    if (j + 1 < jn) step(IC<1>{}, j + 1);
-    t += jn;
-    for (; t < nsteps; ++t) step_barrier();
-    flush(IC<0>{});
-    if constexpr (KI > 1) flush(IC<1>{});
-}
-
 // One pass of the row-streaming pipeline over the rows of `rm` with n inner TV iterations
 // (front / stage / back roles, one barrier per step).  Inlined at two call sites: the main
 // pass and the rare early-stop recompute, each with its own register allocation.
 // GEN: the row pitch is not the image width (rows padded: W % 4 != 0) -- the last-column, norm
 // handling of such rows, compiled only into the kernels that need it
-template <bool EXACT, bool ALPHA1, bool GEN, bool HALF, bool MRG>
+template <bool EXACT, bool ALPHA1, bool GEN, bool HALF>
 __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA1>& sh, const RowMap& rm, const int n,
                                             const bool track, const long long step, const bool fresh) {
     const int lane = threadIdx.x & (WAVE - 1);
@@ -715,32 +529,12 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
     // drains hbot - 1 steps earlier (no change without a bottom halo).
     const int Qb = Q - rm.hbot;
     auto stage_rows = [&](int k) { return min(Q, Qb + n - k + 1); };
-    // Stage waves: classic layout (16 waves) one inner iteration each, wave s = iteration s + 1; merged layout
-    // (MRG, 12 waves: 4 front, SP_MRG_STW stage, 2 back) the first n - SP_MRG_STW stage waves run two
-    // iterations each, the others one.  Stage wave s starts (its lookahead row 0) at step 2 + s + 2 k0(s) and
-    // writes its last iteration's row q at that + 2 cnt + q; the back takes row q at T_back + q.
-    const int nstw_max = MRG ? SP_MRG_STW : SP_MAXST;
-    const int nmrg = MRG ? max(0, n - SP_MRG_STW) : 0;    // stage waves with two iterations (n <= 2 SP_MRG_STW)
-    const int nstw = n - nmrg;                            // stage waves in use
-    auto st_k0 = [&](int s_) { return s_ < nmrg ? 2 * s_ + 1 : 2 * nmrg + (s_ - nmrg) + 1; };
-    auto st_cnt = [&](int s_) { return s_ < nmrg ? 2 : 1; };
-    const int t_back = 4 + 2 * n + nstw;
-    int nsteps = max(Q + 4, Qb + t_back);
-    for (int s_ = 0; s_ < nstw; ++s_) {
-        const int k0 = st_k0(s_), cnt = st_cnt(s_);
-        nsteps = max(nsteps, 2 + s_ + 2 * k0 + 2 * (cnt - 1) + stage_rows(k0 + cnt - 1) + 2);
-    }
-    // classic: 16 waves, back waves right after the n stage waves; MRG: 12 waves, back waves 4 + SP_MRG_STW ..;
-    // waves beyond the pipeline only keep the barrier count
-    int role;
-    if (MRG) {
-        const int s_ = w - SP_FRONT;
-        role = (w < SP_FRONT) ? 0 : (s_ < nstw_max ? (s_ < nstw ? 1 : 3) : (s_ < nstw_max + SP_BACK ? 2 : 3));
-    } else {
-        role = (w < SP_FRONT) ? 0 : (w < SP_FRONT + n ? 1 : (w < SP_FRONT + n + SP_BACK ? 2 : 3));
-    }
+    int nsteps = max(Q + 4, Qb + 4 + 3 * n);
+    for (int k = 1; k <= n; ++k) nsteps = max(nsteps, stage_rows(k) + 3 + 3 * k);
+    // 16 waves always; waves beyond the pipeline (n < 10) only keep the barrier count
+    const int role = (w < SP_FRONT) ? 0 : (w < SP_FRONT + n ? 1 : (w < SP_FRONT + n + SP_BACK ? 2 : 3));
 
-    const int k_st = w - SP_FRONT + 1;                 // inner TV iteration (1-based; classic layout)
+    const int k_st = w - SP_FRONT + 1;                 // inner TV iteration (1-based)
     const bool trk = track && role == 1 && (k_st - 1) >= 2 && (k_st - 1) <= n - 2;
     // Each role runs its own loop (its state is live only there); every wave executes
     // exactly nsteps barriers, so the s_barrier instances pair up across roles.
@@ -869,27 +663,6 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
         const int lastk = W - 1 - gj0;                    // in 0..3 on the lane holding column W-1
         const int nreal = min(CPL, max(0, W - gj0));      // real (non-pitch-padding) columns of the lane
         __builtin_amdgcn_s_setprio(1);
-        if (MRG) {
-            const int s_ = w - SP_FRONT, k0 = st_k0(s_), tb = 2 + s_ + 2 * k0;
-            auto tk = [&](int k) { return track && (k - 1) >= 2 && (k - 1) <= n - 2 ? 1 : 0; };
-            if (st_cnt(s_) == 2) {
-                const int m = tk(k0) | (tk(k0 + 1) << 1);
-#define PSGLA_SLM(F, M) stage_loop_m<EXACT, GEN, ALPHA1, F, HALF, 2, M>(a, sh, rm, k0, n, nsteps, tb, lane, lastk, nreal, core, fresh)
-                if (ALPHA1 && k0 == 1) PSGLA_SLM(true, 0);
-                else if (m == 0) PSGLA_SLM(false, 0);
-                else if (m == 1) PSGLA_SLM(false, 1);
-                else if (m == 2) PSGLA_SLM(false, 2);
-                else PSGLA_SLM(false, 3);
-#undef PSGLA_SLM
-            } else {
-#define PSGLA_SLM(F, M) stage_loop_m<EXACT, GEN, ALPHA1, F, HALF, 1, M>(a, sh, rm, k0, n, nsteps, tb, lane, lastk, nreal, core, fresh)
-                if (ALPHA1 && k0 == 1) PSGLA_SLM(true, 0);
-                else if (tk(k0)) PSGLA_SLM(false, 1);
-                else PSGLA_SLM(false, 0);
-#undef PSGLA_SLM
-            }
-            return;
-        }
         const int qk = stage_rows(k_st);
         if (ALPHA1 && k_st == 1) stage_loop<EXACT, false, GEN, ALPHA1, true, HALF>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core, fresh);
         else if (trk) stage_loop<EXACT, true, GEN, ALPHA1, false, HALF>(a, sh, rm, k_st, n, nsteps, qk, lane, lastk, nreal, core, fresh);
@@ -898,7 +671,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
         for (int t = 0; t < nsteps; ++t) step_barrier();
     } else {
         // ---------------- BACK state ----------------
-        const int bw = w - SP_FRONT - (MRG ? nstw_max : n);   // back wave id (stream rows q % 2 == bw)
+        const int bw = w - SP_FRONT - n;                   // back wave id (stream rows q % 2 == bw)
         // issue priority: back > stages > front.  The back waves are the youngest of the
         // workgroup (lowest age priority) yet close every step (its last arrivals, measured);
         // raising them, then the stages, cut the step by 9 % (A/B).
@@ -947,11 +720,11 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
         back_issue(bw + 2, rc_dma);
         int c1 = 2, c2 = 0;
         // ======================= BACK =======================
-        // Row q (q % 2 == bw) leaves the pipeline at step q + t_back (stage n wrote ring n row q in the step
+        // Row q (q % 2 == bw) leaves the pipeline at step q + 4 + 3n (stage n wrote ring n row q in the step
         // before); its accumulator / sample stores go out in the wave's next step.  Unrolled by those two
         // steps (a step barrier after each), so no step decides at run time whether it has a row.
         int t = 0;
-        const int t0 = t_back + bw;
+        const int t0 = 4 + 3 * n + bw;
         for (; t < t0 && t < nsteps; ++t) step_barrier();
         for (int q = bw; q < Qb && t < nsteps; q += 2) {
             {
@@ -1044,8 +817,8 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
     // early-stop test, per chain); the tracking stages wrote sh.red[segment][k - 1]
 }
 
-template <bool EXACT, bool ALPHA1, bool GEN, bool HALF, bool MRG>
-__global__ void __launch_bounds__(MRG ? SP_MRG_THREADS : TV_THREADS) tv_stream_kernel(const TvArgs a) {
+template <bool EXACT, bool ALPHA1, bool GEN, bool HALF>
+__global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     __shared__ StreamSharedT<ALPHA1> sh;
     __shared__ int s_stop[MAXG];
     __shared__ int s_flag, s_item, s_next;
@@ -1055,7 +828,7 @@ __global__ void __launch_bounds__(MRG ? SP_MRG_THREADS : TV_THREADS) tv_stream_k
     {
         RowMap rm;
         build_rowmap(a, blockIdx.x, rm);
-        stream_pass<EXACT, ALPHA1, GEN, HALF, MRG>(a, sh, rm, a.n_tv, true, step, fresh);
+        stream_pass<EXACT, ALPHA1, GEN, HALF>(a, sh, rm, a.n_tv, true, step, fresh);
         if (!a.fin_inline) return;        // main-pass-only launch (kernel timing): no side effects
         // rel_err partial sums of this stream -> global, per segment's chain (deepinv's
         // early-stop test, per chain); the tracking stages wrote sh.red[segment][k - 1]
@@ -1136,7 +909,7 @@ __global__ void __launch_bounds__(MRG ? SP_MRG_THREADS : TV_THREADS) tv_stream_k
         // the virtual plane (plane, column segment); HALF: the item alone, in both half-waves
         plane_rowmap(a.H, HALF ? a.st_nvp + item : item, rm);
         const int nstop = __builtin_amdgcn_readfirstlane(s_stop[plane / C]);
-        stream_pass<EXACT, ALPHA1, GEN, HALF, MRG>(a, sh, rm, nstop, false, step, fresh);
+        stream_pass<EXACT, ALPHA1, GEN, HALF>(a, sh, rm, nstop, false, step, fresh);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < a.B * a.n_tv * 2; i += blockDim.x) a.norms[i] = 0.0;
@@ -1148,12 +921,8 @@ __global__ void __launch_bounds__(MRG ? SP_MRG_THREADS : TV_THREADS) tv_stream_k
 }
 
 void launch_stream(const TvArgs& s, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen, bool half) {
-    const bool mrg = s.st_merged != 0;
 #define PSGLA_STREAM(E, A, G, HF) \
-    if (exact == E && alpha1 == A && gen == G && half == HF) { \
-        if (mrg) hipLaunchKernelGGL((tv_stream_kernel<E, A, G, HF, true>), grid, dim3(SP_MRG_THREADS), 0, st, s); \
-        else hipLaunchKernelGGL((tv_stream_kernel<E, A, G, HF, false>), grid, dim3(TV_THREADS), 0, st, s); \
-        return; }
+    if (exact == E && alpha1 == A && gen == G && half == HF) { hipLaunchKernelGGL((tv_stream_kernel<E, A, G, HF>), grid, dim3(TV_THREADS), 0, st, s); return; }
     PSGLA_STREAM(true, true, false, false) PSGLA_STREAM(true, true, true, false) PSGLA_STREAM(true, false, false, false) PSGLA_STREAM(true, false, true, false)
     PSGLA_STREAM(false, true, false, false) PSGLA_STREAM(false, true, true, false) PSGLA_STREAM(false, false, false, false) PSGLA_STREAM(false, false, true, false)
     PSGLA_STREAM(true, true, true, true) PSGLA_STREAM(true, false, true, true) PSGLA_STREAM(false, true, true, true) PSGLA_STREAM(false, false, true, true)
