@@ -71,6 +71,10 @@ def parse():
     p.add_argument("--exact", action="store_true", help="bit-exact (IEEE div/sqrt) TV kernel")
     p.add_argument("--kernel-iters", type=int, default=50)
     p.add_argument("--tv-iters", type=int, default=10, help="TV n_it_max (analysis only; the workload is 10)")
+    p.add_argument("--tv-tol", type=float, default=1e-5, help="TV early-stop tolerance (analysis only; the workload "
+                   "is deepinv's 1e-5, where the stop never fires; a large value makes it fire every step)")
+    p.add_argument("--serial-redo", action="store_true", help="early-stop recompute by the finalising workgroup "
+                   "alone (the pre-ABI-11 path; analysis only)")
     p.add_argument("--stream-wgs", type=int, default=0, help="stream kernel work split (0 auto, -1 per plane)")
     p.add_argument("--stream-windows", choices=["auto", "whole", "half"], default="auto",
                    help="stream kernel column windows (auto: half-wave windows where they idle fewer lanes; "
@@ -237,7 +241,8 @@ def main():
     n_iter = w_eager + gs + args.steps + 8
     eng = FusedTvChains(init.contiguous(), y.contiguous(), mask_2d.to(torch.uint8), c1=c1f, c2=c2f,
                         sigma2=float(np.float32(sigma1 ** 2)), alpha=1.0, ths=float(np.float32(s)),
-                        tv=K.TvConstants(n_it_max=args.tv_iters), seed=0, n_iter=n_iter + args.kernel_iters,
+                        tv=K.TvConstants(n_it_max=args.tv_iters, tol=args.tv_tol), seed=0,
+                        n_iter=n_iter + args.kernel_iters, parallel_redo=not args.serial_redo,
                         n_inter=n_inter, n_inter_mmse=nm, chain0=c0, exact=args.exact,
                         stream_wgs=args.stream_wgs, kernel_variant=args.variant, stream_windows=args.stream_windows)
     # warm-up: eager steps + graph capture + one replay
@@ -279,6 +284,7 @@ def main():
     ev0.record()
     eng.replay(reps)
     eng.step(rem)
+    eng.settle()                                     # the last step's early-stop redo, if one is pending
     ev1.record()
     torch.cuda.synchronize()
     barrier()
@@ -329,7 +335,7 @@ def main():
             pj = json.load(open(pmc_json))
             if (pj.get("kernel") == kname and pj.get("workload", {}).get("chains_per_gpu") in (None, B)
                     and pj.get("exact", False) == args.exact
-                    and args.tv_iters == 10 and (H, W) == (256, 256)):
+                    and args.tv_iters == 10 and args.tv_tol == 1e-5 and (H, W) == (256, 256)):
                 traffic = pj.get("hbm_bytes_per_launch")
                 traffic_info = {"traffic_source": os.path.relpath(pmc_json, REPO),
                                 "traffic_commit": pj.get("commit"),
@@ -367,6 +373,7 @@ def main():
                        "global_batch": total_chains, "chains_per_gpu": B, "image": [C, H, W],
                        "parallelism": f"chains{world}", "graph_steps": gs,
                        "kernel_mode": "exact" if args.exact else "fast",
+                       "tv_tol": args.tv_tol, "early_stop_redo": "serial" if args.serial_redo else "parallel",
                        "batch_steps_per_s": round(steps / dt, 2)},
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PSGLA_HIP_ABI_VERSION 10
+#define PSGLA_HIP_ABI_VERSION 11
 
 /* Max inner TV iterations the fused (temporally blocked) kernel handles. */
 #define PSGLA_TV_MAX_FUSED_IT 24
@@ -85,6 +85,13 @@ typedef struct PsglaSchedule {
  *     band kernel (tv_main_kernel) followed by a small finaliser kernel
  *     (tv_finalise_kernel, <= 8 workgroups) that does the same.
  * launch_mask 1 launches only the main pass of either variant (timing).
+ * deepinv's early stop (rare at the reference's settings) in the row stream with a `redo` buffer (ABI 11) and a
+ * grid the CUs hold at once: the step's finaliser only records which chains stopped (redo[4 + g] = their
+ * inner-iteration count, redo[0] = pending); the NEXT launch's workgroups first redo the stopped chains' part of
+ * that step -- every workgroup its own rows, all in parallel --, meet at one grid barrier (redo[1]), then run their
+ * own step.  A run's last step is settled by launch_mask 4 (the pending redo alone, then redo[0] cleared), which
+ * the host issues before it reads results.  Without `redo` (or with a larger grid), and in the tile kernel, the
+ * finaliser's workgroup recomputes the stopped chains itself, one (plane, segment) / tile after another.
  * ------------------------------------------------------------------------------- */
 typedef struct PsglaTvStep {
     int32_t B, C, H, W;
@@ -115,7 +122,8 @@ typedef struct PsglaTvStep {
                                  the other workgroups' stores (a guard that should never expire:
                                  the host checks it, FusedTvChains.check_handoff)               */
     int32_t launch_mask;      /* 0 or 3: both kernels; 1: tile kernel only (re-runs the same step:
-                                 idempotent, for kernel timing); 2: finaliser only            */
+                                 idempotent, for kernel timing); 2: finaliser only; 4 (ABI 11): settle a
+                                 pending early-stop redo of the last step (no step is run)     */
     int32_t kernel_variant;   /* 0: auto (see above); 1: force the band kernel; 2: force the row stream
                                  (one row per pipeline step); 4: force the small-batch tile kernel
                                  (ldw % 4 == 0).  Other values (3 included: the row-pair pipeline
@@ -138,6 +146,9 @@ typedef struct PsglaTvStep {
                                  256-column windows would leave a third of the lanes idle); 1 whole
                                  256-column windows only; 2 half-wave windows whenever they fit
                                  (diagnostic: the halo cost of 128-column pipelines at any width)  */
+    int32_t* redo;            /* (ABI 11) device int[4 + B], zero-initialised, or NULL: the parallel early-stop
+                                 redo (above): [0] pending (bit 0) and the stopped step's TV restart flag
+                                 (bit 1), [1] the grid-barrier count, [4 + g] chain g's inner iterations  */
 } PsglaTvStep;
 
 int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream);

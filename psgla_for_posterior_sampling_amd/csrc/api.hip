@@ -125,6 +125,27 @@ template <bool EXACT, int FRONT, bool ALPHA1>
 static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
     const int P = a.B * a.C;
     if (mask == 0) mask = 3;
+    // launch_mask 4: settle a pending early-stop redo of the last step (the kernel redoes the stopped chains' part
+    // of it, nothing else), then clear the pending flag; only the stream / tile kernels with a redo buffer have one
+    if (mask == 4) {
+        if (FRONT != FRONT_INPAINT || !a.redo || (a.tile_r == 0 && !a.stream)) return 0;
+        TvArgs s = a;
+        s.fin_inline = 0;
+        s.redo_only = 1;
+        int rc;
+        if (a.tile_r > 0) {
+            return 0;                    // (the tile kernel's finaliser recomputes stopped chains itself)
+        } else {
+            const int grid = s.split_wgs > 0 ? s.split_wgs : s.st_nvp;
+            s.par_redo = grid <= device_cus() ? 1 : 0;
+            if (!s.par_redo) return 0;
+            launch_stream(s, dim3(grid), st, EXACT, ALPHA1, !(s.ldw == s.W && s.st_nsegs == 1), s.st_half != 0);
+            rc = launch_check("tv_stream_kernel(redo)");
+        }
+        if (rc) return rc;
+        if (hipMemsetAsync(a.redo, 0, sizeof(int), st) != hipSuccess) return launch_check("psgla_tv_step(redo clear)");
+        return 0;
+    }
     if (mask & 1) {
         if (FRONT == FRONT_INPAINT && a.tile_r > 0) {
             TvArgs s = a;
@@ -136,6 +157,7 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
             // reads issued back to back (round 4), 8 copies cost 8 chains of 30 tiles +1.6 % and save castle at
             // batch 2 (108 tiles per chain) 3.5 % and at batch 1 (246) 5 % (profiles/r04k_tile_fin_ab.txt)
             if (s.norm_copies < 1 || s.C * s.nbands * s.st_nsegs < 64) s.norm_copies = 1;
+            s.par_redo = 0;              // the tile kernel recomputes stopped chains in its finalising workgroup
             const bool gen = !(s.ldw == s.W && s.st_nsegs == 1);
             if (launch_tile(s, dim3(grid), st, EXACT, ALPHA1, gen)) return launch_check("tv_tile_kernel");
             return fail(0, "psgla_tv_step: internal error: no tile kernel of this shape");
@@ -144,6 +166,7 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
             TvArgs s = a;
             s.fin_inline = (mask & 2) ? 1 : 0;
             const int grid = s.split_wgs > 0 ? s.split_wgs : s.st_nvp;   // virtual planes
+            s.par_redo = (s.redo && grid <= device_cus()) ? 1 : 0;         // (one workgroup per CU: LDS)
             const bool gen = !(s.ldw == s.W && s.st_nsegs == 1);
             launch_stream(s, dim3(grid), st, EXACT, ALPHA1, gen, s.st_half != 0);
             int rc = launch_check("tv_stream_kernel");
@@ -310,6 +333,8 @@ int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream) {
     a.n_inter = s->n_inter; a.nm = s->n_inter_mmse; a.coef = s->acc_coef;
     a.samples = s->samples; a.samples_cap = s->samples_cap;
     a.blocks = s->blocks; a.blocks2 = s->blocks2; a.blocks_cap = s->blocks_cap;
+    a.redo = d->redo;
+    if (d->launch_mask < 0 || d->launch_mask > 4) return fail(0, "psgla_tv_step: launch_mask must be 0 .. 4");
     if (select_step_kernel(d, a) < 0) return g_sel_err == g_err ? (int)hipErrorInvalidValue : fail(0, g_sel_err);
     hipStream_t st = (hipStream_t)stream;
     const int m = d->launch_mask;

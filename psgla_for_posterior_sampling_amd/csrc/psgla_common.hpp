@@ -130,7 +130,44 @@ struct TvArgs {
     int tile_r;                     // > 0: small-batch tile kernel with tile_r rows per wave (one tile per workgroup)
     int tile_nw;                    // tile kernel: waves per workgroup (16 or 8)
     int norm_copies;                // tile kernel: copies of norms its rel-err sums are spread over (>= 1)
+    int* redo;                      // stream / tile kernel: parallel early-stop redo state (PsglaTvStep.redo) or null
+    int par_redo;                   // 1: the redo runs in parallel in the next launch (grid resident at once)
+    int redo_only;                  // 1: settle a pending redo only (launch_mask 4)
 };
+
+// The launch's step index and TV restart flag, wave-uniform by construction (readfirstlane: code that stores to
+// global memory before using them must not make the compiler treat them as per-lane values)
+__device__ __forceinline__ long long launch_step(const TvArgs& a) {
+    const long long v = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
+    const int lo = __builtin_amdgcn_readfirstlane((int)(v & 0xFFFFFFFFLL));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ bool launch_fresh(const TvArgs& a) {
+    return __builtin_amdgcn_readfirstlane(a.fresh_dev ? *a.fresh_dev : a.fresh_host) != 0;
+}
+
+// Grid-wide barrier of a launch whose workgroups are all resident (the parallel early-stop redo only): each
+// workgroup's stores drained and released (agent scope), one arrival per workgroup on *cnt, a bounded poll, an
+// agent acquire (MI355X_MICROARCH.md, valid hand-off form).  An expired guard is recorded in *guard for the host.
+__device__ __forceinline__ void grid_sync(int* cnt, int* guard) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool done = false;
+        for (int spin = 0; spin < (1 << 24) && !done; ++spin) {
+            done = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (int)gridDim.x;
+            if (!done) __builtin_amdgcn_s_sleep(2);
+        }
+        if (!done) __hip_atomic_store(guard, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
 
 // Inner iterations (chunk-local) whose rel_err deepinv tests: global index >= 2 ("it > 1"); in the call's
 // last chunk not the last iteration (stopping there changes nothing)

@@ -817,14 +817,57 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
     // early-stop test, per chain); the tracking stages wrote sh.red[segment][k - 1]
 }
 
+// The previous step's pending early-stop redo (rare; a.redo[0], set by that step's finaliser): this workgroup
+// redoes, segment by segment, every segment of its row range whose chain stopped (a.redo[4 + g] < n_tv inner
+// iterations) -- each segment with its halo rows as the main pass cut them, so the workgroups' core rows cover
+// every stopped row once (HALF: each item of a pair alone, in both half-waves, as the serial recompute).  The
+// redone step's inputs are intact (ping-pong state).  (Folding the redo into the main pass's call site, in a loop,
+// measured +14 % per step: the loop keeps the row map live across the pipeline.)
+template <bool EXACT, bool ALPHA1, bool GEN, bool HALF>
+__device__ __forceinline__ void stream_redo(const TvArgs& a, StreamSharedT<ALPHA1>& sh, long long pstep, bool pfresh) {
+    RowMap rm;
+    build_rowmap(a, blockIdx.x, rm);
+    const int nitems = a.B * a.C * a.st_nsegs;
+    for (int s = 0; s < rm.ns; ++s) {
+        for (int hh = 0; hh < (HALF ? 2 : 1); ++hh) {
+            const int item = HALF ? 2 * rm.pl(s) + hh : rm.pl(s);
+            if (item >= nitems) continue;
+            const int nstop = __builtin_amdgcn_readfirstlane(a.redo[4 + (item / a.st_nsegs) / a.C]);
+            if (nstop >= a.n_tv) continue;
+            RowMap r1;
+            r1.ns = 1;
+            r1.Q = rm.qs(s + 1) - rm.qs(s);
+            r1.htop = s == 0 ? rm.htop : 0;
+            r1.hbot = s == rm.ns - 1 ? rm.hbot : 0;
+            r1.q1 = r1.q2 = r1.q3 = r1.Q;
+            r1.pl0 = HALF ? a.st_nvp + item : item;
+            r1.pl1 = r1.pl2 = r1.pl3 = 0;
+            r1.lo0 = rm.lo(s);
+            r1.lo1 = r1.lo2 = r1.lo3 = 0;
+            __syncthreads();
+            stream_pass<EXACT, ALPHA1, GEN, HALF>(a, sh, r1, nstop, false, pstep, pfresh);
+        }
+    }
+}
+
 template <bool EXACT, bool ALPHA1, bool GEN, bool HALF>
 __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     __shared__ StreamSharedT<ALPHA1> sh;
     __shared__ int s_stop[MAXG];
     __shared__ int s_flag, s_item, s_next;
     const int C = a.C;
-    const long long step = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
-    const bool fresh = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
+    const long long step = launch_step(a);
+    const bool fresh = launch_fresh(a);
+    // the previous step's pending early-stop redo (rare): all workgroups in parallel, then one grid barrier;
+    // launch_mask 4 (redo_only): the redo alone
+    if (a.par_redo && (a.fin_inline || a.redo_only)) {
+        const int pend = __builtin_amdgcn_readfirstlane(a.redo[0]);
+        if (pend & 1) {
+            stream_redo<EXACT, ALPHA1, GEN, HALF>(a, sh, step - 1, (pend & 2) != 0);
+            if (!a.redo_only) grid_sync(a.redo + 1, a.arrive + 3);
+        }
+        if (a.redo_only) return;
+    }
     {
         RowMap rm;
         build_rowmap(a, blockIdx.x, rm);
@@ -886,6 +929,17 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
         const int m = s_stop[g];
         s_stop[g] = m ? (__ffs(m) - 1) + 1 : a.n_tv;
         if (m) s_item = 1;                    // some chain stopped early (benign race: all write 1)
+    }
+    __syncthreads();
+    if (a.par_redo) {
+        // parallel redo (next launch, or launch_mask 4): publish the stop counts and the pending flag, reset the
+        // grid-barrier count (every workgroup of this launch passed it before its main pass)
+        for (int g = threadIdx.x; g < G; g += blockDim.x) a.redo[4 + g] = s_stop[g];
+        if (threadIdx.x == 0) {
+            a.redo[1] = 0;
+            a.redo[0] = s_item ? (1 | (fresh ? 2 : 0)) : 0;
+        }
+        s_next = 1 << 30;                     // (uniform: every thread writes it) no serial recompute
     }
     __syncthreads();
     if (s_item == 0) s_next = 1 << 30;        // common case: nothing to redo, skip the scan

@@ -365,8 +365,8 @@ template <bool EXACT, bool ALPHA1, int R, bool GEN, int NW>
 __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
     __shared__ TileShared<R, NW> sh;
     constexpr bool SPLIT = NW == 8;                    // two-phase arrival (below)
-    const long long step = (a.d_step ? *a.d_step : 0LL) + a.step_offset;
-    const bool fresh = a.fresh_dev ? (*a.fresh_dev != 0) : (a.fresh_host != 0);
+    const long long step = launch_step(a);
+    const bool fresh = launch_fresh(a);
     const int P = a.B * a.C;
     const int T = a.nbands * (GEN ? a.st_nsegs : 1);  // tiles per plane: (column segment, band)
     {

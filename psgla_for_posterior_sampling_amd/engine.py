@@ -29,7 +29,7 @@ class FusedTvChains:
                  n_inter: int, n_inter_mmse: int, chain0: int = 0, exact: bool = False,
                  tv_x2: torch.Tensor | None = None, tv_u2: torch.Tensor | None = None,
                  store_samples: bool = True, store_blocks: bool = True, kernel_variant: str = "auto",
-                 stream_wgs: int = 0, stream_windows: str = "auto"):
+                 stream_wgs: int = 0, stream_windows: str = "auto", parallel_redo: bool = True):
         if init.dim() != 4:
             raise ValueError("init must be (B, C, H, W)")
         if tv.n_it > N.TV_MAX_FUSED_IT:
@@ -102,7 +102,11 @@ class FusedTvChains:
         if stream_windows not in ("auto", "whole", "half"):
             raise ValueError("stream_windows must be 'auto', 'whole' or 'half'")
         d.stream_windows = {"auto": 0, "whole": 1, "half": 2}[stream_windows]
+        # deepinv's early stop, when it fires, is redone in parallel by the next launch (include/psgla_hip.h); the
+        # last step's pending redo is settled (launch_mask 4) before results are read: settle()
+        d.redo = self.work.redo.data_ptr() if parallel_redo else None
         self.desc = d
+        self._unsettled = False
         self.sched_struct = self.sched.struct(True, 0)
         if self.warm_first:
             # first step of a warm-started run: the TV primal x2 (previous run's state) is not X
@@ -139,9 +143,25 @@ class FusedTvChains:
                 raise RuntimeError("all n_iter steps already done")
             if self.steps_done == 0 and self.warm_first:
                 self._launch(self.desc_first)
-            else:
-                self._launch(self.desc)
+                self.steps_done += 1
+                # a warm-started first step reads the previous run's TV primal (desc_first's x2): its redo, if any,
+                # must run with that descriptor, not with the next step's
+                self._unsettled = True
+                self.settle(self.desc_first)
+                continue
+            self._launch(self.desc)
             self.steps_done += 1
+            self._unsettled = True
+
+    def settle(self, desc=None):
+        """Apply a pending early-stop redo of the last step (launch_mask 4: the stopped chains' part of that
+        step, recomputed in parallel; nothing when no chain stopped).  Every result accessor calls it."""
+        desc = self.desc if desc is None else desc
+        if self._unsettled and desc.redo:
+            d = N.PsglaTvStep.from_buffer_copy(desc)
+            d.launch_mask = 4
+            self._launch(d)
+        self._unsettled = False
 
     def capture(self, steps_per_graph: int):
         """Capture `steps_per_graph` identical steps into one hipGraph (after step 0): one launch per
@@ -164,6 +184,7 @@ class FusedTvChains:
                 raise RuntimeError("replay would exceed n_iter")
             self.graph.replay()
             self.steps_done += self.graph_steps
+            self._unsettled = True
 
     def rewind(self, step: int):
         """Set the step index (device counter, stream-ordered, and host count) back to `step`, which
@@ -173,6 +194,7 @@ class FusedTvChains:
         step = int(step)
         if step < 0 or (step - self.steps_done) % 2:
             raise ValueError("rewind target must be >= 0 and of the current step's parity")
+        self.settle()                     # a pending redo belongs to the step before the rewind
         self.sched.d_step.fill_(step)
         self.steps_done = step
 
@@ -180,6 +202,7 @@ class FusedTvChains:
         """Device copies of everything a step reads or advances (chain / TV state, live accumulators, the
         step counter, the TV restart flag) -- for benchmarking: replays after a snapshot can be undone by
         restore() (samples / block means already written stay written)."""
+        self.settle()
         torch.cuda.current_stream().synchronize()
         bufs = {"x": self.x, "u2": self.u2, "mean": self.mean, "sq": self.sq}
         if self.x2 is not None:
@@ -198,7 +221,9 @@ class FusedTvChains:
                     dst.copy_(src)
         self.sched.d_step.copy_(snap["d_step"])
         self.work.fresh.copy_(snap["fresh"])
+        self.work.redo.zero_()            # snapshots are settled: nothing pending
         self.steps_done = snap["steps_done"]
+        self._unsettled = False
 
     @property
     def main_kernel(self) -> str:
@@ -234,16 +259,19 @@ class FusedTvChains:
         self.step(n)
 
     def check_handoff(self):
-        """Raise if the tile kernel's early-stop recompute ever gave up waiting for the other workgroups'
-        stores (arrive[3], include/psgla_hip.h; a guard that should never expire -- if it did, the
-        recomputed chains may have been overwritten by late first-pass stores).  One host sync."""
+        """Raise if an early-stop recompute ever gave up waiting for the other workgroups (arrive[3],
+        include/psgla_hip.h: the tile kernel's serial recompute waiting for their stores, or the parallel redo's
+        grid barrier; guards that should never expire -- if one did, the recomputed chains may have raced the
+        other workgroups' stores).  One host sync."""
+        self.settle()
         if int(self.work.arrive[3].item()) != 0:
-            raise RuntimeError("tv_tile_kernel: early-stop recompute hand-off guard expired; results of the "
-                               "recomputed chains are not trustworthy")
+            raise RuntimeError("early-stop recompute hand-off guard expired (tv_stream_kernel / tv_tile_kernel); "
+                               "results of the recomputed chains are not trustworthy")
 
     # -- results --------------------------------------------------------------------
     @property
     def X(self) -> torch.Tensor:
+        self.settle()
         return self._view(self.x[self.steps_done & 1])
 
     def input_state(self, step: int) -> torch.Tensor:
@@ -254,21 +282,25 @@ class FusedTvChains:
 
     @property
     def u2_state(self) -> torch.Tensor:
+        self.settle()
         return self._view(self.u2[self.steps_done & 1], u2=True)
 
     @property
     def x2_state(self) -> torch.Tensor:
         if self.alpha1:
             return self.X
+        self.settle()
         return self._view(self.x2[self.steps_done & 1])
 
     def samples(self):
+        self.settle()
         if self.sched.samples is None:
             return None
         k = self.sched.n_samples_done(self.steps_done)
         return self._view(self.sched.samples[:k])
 
     def blocks(self):
+        self.settle()
         k = self.sched.n_blocks_done(self.steps_done)
         if self.sched.blocks is None:
             return None, None

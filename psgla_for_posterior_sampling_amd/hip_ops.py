@@ -362,3 +362,5 @@ class TvWorkspace:
         self.norms = self.norms_all[:max(groups, 1)]
         self.arrive = torch.zeros(4, dtype=torch.int32, device=device)
         self.fresh = torch.zeros(4, dtype=torch.int32, device=device)
+        # parallel early-stop redo state (PsglaTvStep.redo, ABI 11): [0] pending, [1] grid barrier, [4 + g] stop counts
+        self.redo = torch.zeros(4 + max(groups, 1), dtype=torch.int32, device=device)

@@ -951,3 +951,42 @@ def test_tile_kernel_early_stop_handoff_full_size(B, H, W, tol):
     for a, b in zip(outs[("stream", tol)], outs[("tile", tol)]):
         assert torch.equal(a, b)
     assert not torch.equal(outs[("tile", tol)][3], outs[("tile", 1e-5)][3]), "no early stop fired"
+
+
+@pytest.mark.parametrize("B,H,W,variant,stream_wgs", [(64, 256, 256, "stream", 0), (64, 481, 321, "stream", 0),
+                                                       (6, 40, 52, "stream", -1), (8, 256, 256, "tile", 0),
+                                                       (1, 481, 321, "tile", 0)])
+def test_parallel_early_stop_redo_equals_serial(B, H, W, variant, stream_wgs):
+    """ABI 11: when deepinv's early stop fires in the row stream, the next launch's workgroups redo the stopped
+    chains' part of the step in parallel (each its own rows, then a grid barrier), the run's last step through
+    launch_mask 4; the finaliser's serial recompute (no redo buffer) is the reference.  (The tile kernel keeps the
+    serial recompute with or without the buffer: its cases check that the buffer changes nothing there.)  tol = 0.2 makes the stop fire on every
+    chain in every step (after 3 inner iterations), tol = 2e-3 on some steps only; fast kernels, hipGraph replay,
+    the bench shape (64 chains: row split, 256 workgroups), the castle shape at 64 chains (half-wave windows,
+    segments), per-plane streams, the 8-chain tile kernel and castle at batch 1: bit-identical."""
+    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    g = torch.Generator(device=DEV).manual_seed(5)
+    xs = torch.rand((B, 3, H, W), generator=g, device=DEV)
+    gen = torch.Generator(device=DEV).manual_seed(0)
+    mask2d = (torch.rand((H, W), generator=gen, device=DEV) > 0.5).to(torch.uint8)
+    y = mask2d.float() * xs
+    init = (mask2d.float() * y + (1 - mask2d.float()) * 0.5).contiguous()
+    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
+    for tol in (0.2, 2e-3):
+        outs = []
+        for par in (True, False):
+            eng = FusedTvChains(init, y.contiguous(), mask2d, c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
+                                alpha=1.0, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10, tol=tol),
+                                seed=1, n_iter=24, n_inter=3, n_inter_mmse=4, kernel_variant=variant,
+                                stream_wgs=stream_wgs, parallel_redo=par)
+            assert eng.main_kernel == "tv_" + variant + "_kernel"
+            eng.run(5)                         # eager steps: each launch redoes the previous step's stops
+            eng.run(19, graph_steps=6)         # graph replays, then eager remainder + settle
+            torch.cuda.synchronize()
+            eng.check_handoff()
+            assert int(eng.work.redo[0].item()) == 0 and int(eng.work.arrive[0].item()) == 0
+            bm, bm2 = eng.blocks()
+            outs.append((eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone()))
+        for a, b in zip(*outs):
+            assert torch.equal(a, b), (tol, B, H, W, variant)
