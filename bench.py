@@ -73,8 +73,6 @@ def parse():
     p.add_argument("--tv-iters", type=int, default=10, help="TV n_it_max (analysis only; the workload is 10)")
     p.add_argument("--tv-tol", type=float, default=1e-5, help="TV early-stop tolerance (analysis only; the workload "
                    "is deepinv's 1e-5, where the stop never fires; a large value makes it fire every step)")
-    p.add_argument("--tile-multi-steps", type=int, default=0, help="small-batch tile kernel: steps per launch in "
-                   "the graph segments (tv_tile_ms_kernel; 0: one step per launch)")
     p.add_argument("--serial-redo", action="store_true", help="early-stop recompute by the finalising workgroup "
                    "alone (the pre-ABI-11 path; analysis only)")
     p.add_argument("--stream-wgs", type=int, default=0, help="stream kernel work split (0 auto, -1 per plane)")
@@ -245,7 +243,6 @@ def main():
                         sigma2=float(np.float32(sigma1 ** 2)), alpha=1.0, ths=float(np.float32(s)),
                         tv=K.TvConstants(n_it_max=args.tv_iters, tol=args.tv_tol), seed=0,
                         n_iter=n_iter + args.kernel_iters, parallel_redo=not args.serial_redo,
-                        tile_multi_steps=args.tile_multi_steps,
                         n_inter=n_inter, n_inter_mmse=nm, chain0=c0, exact=args.exact,
                         stream_wgs=args.stream_wgs, kernel_variant=args.variant, stream_windows=args.stream_windows)
     # warm-up: eager steps + graph capture + one replay
@@ -331,7 +328,7 @@ def main():
         dist.all_gather_object(placement, here)
 
     traffic, traffic_info = None, None
-    kname = eng.graph_kernel           # the kernel the timed graphs launch (once per step, or per multi-step launch)
+    kname = eng.main_kernel            # the kernel the timed graphs launch, once per step
     pmc_json = args.pmc_json or os.path.join(REPO, PMC_PROFILES.get(kname, "none"))
     if os.path.exists(pmc_json):
         try:

@@ -149,20 +149,12 @@ typedef struct PsglaTvStep {
     int32_t* redo;            /* (ABI 11) device int[4 + B], zero-initialised, or NULL: the parallel early-stop
                                  redo (above): [0] pending (bit 0) and the stopped step's TV restart flag
                                  (bit 1), [1] the grid-barrier count, [4 + g] chain g's inner iterations  */
-    int32_t multi_steps;      /* (ABI 11) > 1: where the small-batch tile kernel runs with 32- or 48-row tiles all
-                                 resident at once, ONE launch runs that many consecutive steps
-                                 (tv_tile_ms_kernel: tiles wait only for their halo neighbours between steps,
-                                 deepinv's per-chain stop with one step of slack) and advances *d_step by as
-                                 many; psgla_tv_step_kernel() answers 5 then.  Otherwise one step per launch. */
-    int32_t* ms_state;        /* (ABI 11) device int[4 + 4 B + 4096], zero-initialised: its launch state        */
-    double* ms_norms;         /* (ABI 11) device double[2][B][n_tv][2], zero-initialised: its rel-err sums      */
 } PsglaTvStep;
 
 int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream);
 /* Which kernel psgla_tv_step launches for this descriptor (host-side query, launches nothing):
  * 0 band kernel + finaliser, 1 row stream (tv_stream_kernel), 3 small-batch tile kernel
- * (tv_tile_kernel), 5 multi-step tile kernel (tv_tile_ms_kernel, multi_steps steps per launch);
- * -1 if the descriptor is rejected.  (2 is unused since ABI 7.) */
+ * (tv_tile_kernel); -1 if the descriptor is rejected.  (2 is unused since ABI 7.) */
 int psgla_tv_step_kernel(const PsglaTvStep* d);
 
 /* ---------------------------------------------------------------------------------

@@ -46,7 +46,7 @@ class PsglaTvStep(ctypes.Structure):
         ("n_tv", c_i32), ("exact", c_i32), ("seed", c_u64), ("chain0", c_i32), ("advance_step", c_i32),
         ("fresh", c_vp), ("norms", c_vp), ("arrive", c_vp), ("launch_mask", c_i32),
         ("kernel_variant", c_i32), ("stream_wgs", c_i32), ("ldw", c_i32), ("norms_copies", c_i32),
-        ("stream_windows", c_i32), ("redo", c_vp), ("multi_steps", c_i32), ("ms_state", c_vp), ("ms_norms", c_vp),
+        ("stream_windows", c_i32), ("redo", c_vp),
     ]
 
 

@@ -121,13 +121,6 @@ static int stream_segments(int W, int L, int h, int* seg_w, int win = TV_COLS) {
     return 0;
 }
 
-// The multi-step tile kernel runs the descriptor's multi_steps steps in one launch: 16-wave tiles of 2 or 3 rows per
-// wave, every tile resident at once (its workgroups wait on each other), its state buffers given.
-static bool ms_eligible(const TvArgs& s, int grid) {
-    return s.ms_steps > 1 && s.ms && s.ms_norms && s.tile_r > 0 && s.tile_nw == 16 && (s.tile_r == 2 || s.tile_r == 3) &&
-           grid <= device_cus() && grid <= 4096;
-}
-
 template <bool EXACT, int FRONT, bool ALPHA1>
 static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
     const int P = a.B * a.C;
@@ -160,13 +153,6 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
             const int grid = P * s.nbands * s.st_nsegs;                   // tile_kernel: one workgroup per tile
             // (the two-phase arrival counter keeps a count of workgroups in 15 bits)
             if (grid > 32767) return fail(0, "psgla_tv_step: more than 32767 tiles in one launch");
-            // multi-step launch (tv_tile_ms_kernel): every tile resident at once, 16-wave tiles, the whole step
-            if (ms_eligible(s, grid) && s.fin_inline) {
-                if (launch_tile_ms(s, dim3(grid), st, EXACT, ALPHA1, !(s.ldw == s.W && s.st_nsegs == 1)))
-                    return launch_check("tv_tile_ms_kernel");
-                return fail(0, "psgla_tv_step: internal error: no multi-step tile kernel of this shape");
-            }
-            s.ms_steps = 1;
             // several copies of the rel-err sums only where many tiles share a chain: with the finaliser's copy
             // reads issued back to back (round 4), 8 copies cost 8 chains of 30 tiles +1.6 % and save castle at
             // batch 2 (108 tiles per chain) 3.5 % and at batch 1 (246) 5 % (profiles/r04k_tile_fin_ab.txt)
@@ -348,9 +334,6 @@ int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream) {
     a.samples = s->samples; a.samples_cap = s->samples_cap;
     a.blocks = s->blocks; a.blocks2 = s->blocks2; a.blocks_cap = s->blocks_cap;
     a.redo = d->redo;
-    a.ms_steps = d->multi_steps > 1 ? d->multi_steps : 1;
-    a.ms = d->ms_state;
-    a.ms_norms = d->ms_norms;
     if (d->launch_mask < 0 || d->launch_mask > 4) return fail(0, "psgla_tv_step: launch_mask must be 0 .. 4");
     if (select_step_kernel(d, a) < 0) return g_sel_err == g_err ? (int)hipErrorInvalidValue : fail(0, g_sel_err);
     hipStream_t st = (hipStream_t)stream;
@@ -370,12 +353,6 @@ int psgla_tv_step_kernel(const PsglaTvStep* d) {
     a.ldw = d->ldw > 0 ? d->ldw : d->W;
     const int k = select_step_kernel(d, a);
     if (k < 0 && g_sel_err != g_err) fail(0, g_sel_err);
-    if (k == 3) {
-        a.ms_steps = d->multi_steps > 1 ? d->multi_steps : 1;
-        a.ms = d->ms_state;
-        a.ms_norms = d->ms_norms;
-        if (ms_eligible(a, a.B * a.C * a.nbands * a.st_nsegs)) return 5;
-    }
     return k;
 }
 

@@ -133,9 +133,6 @@ struct TvArgs {
     int* redo;                      // stream / tile kernel: parallel early-stop redo state (PsglaTvStep.redo) or null
     int par_redo;                   // 1: the redo runs in parallel in the next launch (grid resident at once)
     int redo_only;                  // 1: settle a pending redo only (launch_mask 4)
-    int ms_steps;                   // tile kernel: > 1 = multi-step launch (tv_tile_ms_kernel) of that many steps
-    int* ms;                        // its state (ints, zero between launches) and rel-err sums
-    double* ms_norms;
 };
 
 // The launch's step index and TV restart flag, wave-uniform by construction (readfirstlane: code that stores to
@@ -178,19 +175,6 @@ __device__ __forceinline__ int trk_lo(const TvArgs& a) { return a.it0 >= 2 ? 0 :
 __device__ __forceinline__ int trk_hi(const TvArgs& a) { return a.last_chunk ? a.n_tv - 2 : a.n_tv - 1; }
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-// 16-B load that bypasses L1 (sc1): data another workgroup of the same launch wrote with sc1 stores.  Inline asm
-// without a wait: the caller waits (vmcnt) and then ties the value to that wait (tie4) before using it.
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ f32x4_t ld4_sc1(const float* p) {
-    f32x4_t v;
-    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
-// a value loaded by asm, usable only after the (earlier, volatile) vmcnt wait
-__device__ __forceinline__ float4 tie4(f32x4_t v) {
-    asm volatile("" : "+v"(v));
-    return make_float4(v[0], v[1], v[2], v[3]);
-}
 __device__ __forceinline__ void st4(float* p, float a, float b, float c, float d) {
     *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
 }
@@ -279,11 +263,6 @@ __device__ __forceinline__ void glds16(const void* src, void* dst) {
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
                  :: "v"(src), "s"(off) : "memory", "m0");
 }
-__device__ __forceinline__ void glds16_sc1(const void* src, void* dst) {
-    const unsigned off = (unsigned)(size_t)(lptr_t)dst;
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off sc1"
-                 :: "v"(src), "s"(off) : "memory", "m0");
-}
 __device__ __forceinline__ void glds4(const void* src, void* dst) {
     const unsigned off = (unsigned)(size_t)(lptr_t)dst;
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off"
@@ -362,6 +341,5 @@ template <bool EXACT, int FRONT, bool ALPHA1> void launch_band_main(const TvArgs
 template <bool EXACT, int FRONT, bool ALPHA1> void launch_band_finalise(const TvArgs& a, dim3 grid, hipStream_t st);
 void launch_stream(const TvArgs& a, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen, bool half);
 bool launch_tile(const TvArgs& a, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen);
-bool launch_tile_ms(const TvArgs& a, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen);
 
 }  // namespace psgla

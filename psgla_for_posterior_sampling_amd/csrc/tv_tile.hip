@@ -23,10 +23,6 @@ namespace psgla {
 // interior cuts.
 // ---------------------------------------------------------------------------------------
 
-// commit hook of the single-step kernel: every step is kept
-struct NoCommit { __device__ bool operator()() const { return true; } };
-constexpr NoCommit no_commit{};
-
 template <int R, int NW>
 struct TileShared {
     float4 zrow[NW][WAVE];             // first-row z of each wave (read by the wave above)
@@ -39,15 +35,9 @@ struct TileShared {
 
 // before_u2: called by every wave once the tile's rel-err sums and X side are issued, before its u2 stores
 // (the kernel's main pass: the step's arrival, so the u2 stores drain while the last workgroup finalises)
-// MS (the multi-step kernel, tv_tile_ms_kernel): the state the tile reads was written in this launch by other
-// workgroups, so it is loaded bypassing L1 (sc1: MI355X_MICROARCH.md's hand-off form with sc1 stores and loads);
-// commit() -- called by every thread just before the tile's first store or rel-err add -- returns false when the
-// step must be dropped (the chain's previous step stopped early and is redone first): nothing is then stored and
-// sb_tile returns false.  The rel-err sums go to a.ms_norms[step & 1] (one copy).
-template <bool EXACT, bool ALPHA1, int R, bool GEN, int NW, bool MS = false, typename BeforeU2, typename Commit>
-__device__ __forceinline__ bool sb_tile(const TvArgs& a, TileShared<R, NW>& sh, int plane, int seg, int band, int n_it,
-                                        bool track, long long step, bool fresh, BeforeU2&& before_u2, Commit&& commit) {
-    bool ok = true, decided = false;
+template <bool EXACT, bool ALPHA1, int R, bool GEN, int NW, typename BeforeU2>
+__device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, int plane, int seg, int band, int n_it,
+                                        bool track, long long step, bool fresh, BeforeU2&& before_u2) {
     float x2[R][CPL], u0[R][CPL], u1[R][CPL];
     double* const nrm = a.norms;
     const int lane = threadIdx.x & (WAVE - 1);
@@ -81,7 +71,6 @@ __device__ __forceinline__ bool sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
     bool rv[R], core[R];
     // ---- 1. every load the first iteration needs in flight: state, observation and mask to registers
     float4 fX[R], fY[R], fU0[R], fU1[R], fXS[R];
-    f32x4_t sX[R], sU0[R], sU1[R], sXS[R];         // MS: the state's sc1 loads (tied to a wait before use)
     uint32_t fM[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -92,20 +81,11 @@ __device__ __forceinline__ bool sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
         fM[r] = 0u;
         if (rv[r] && colok) {
             const size_t base = poff + (size_t)gi[r] * L + gj0;
-            if (MS) {
-                sX[r] = ld4_sc1(a.x[par_in] + base);
-                if (!fresh) {
-                    sU0[r] = ld4_sc1(a.u2[par_in] + 2 * base);
-                    sU1[r] = ld4_sc1(a.u2[par_in] + 2 * base + 4);
-                    if (!ALPHA1) sXS[r] = ld4_sc1(a.x2[par_in] + base);
-                }
-            } else {
-                fX[r] = ld4(a.x[par_in] + base);
-                if (!fresh) {
-                    fU0[r] = ld4(a.u2[par_in] + 2 * base);
-                    fU1[r] = ld4(a.u2[par_in] + 2 * base + 4);
-                    if (!ALPHA1) fXS[r] = ld4(a.x2[par_in] + base);
-                }
+            fX[r] = ld4(a.x[par_in] + base);
+            if (!fresh) {
+                fU0[r] = ld4(a.u2[par_in] + 2 * base);
+                fU1[r] = ld4(a.u2[par_in] + 2 * base + 4);
+                if (!ALPHA1) fXS[r] = ld4(a.x2[par_in] + base);
             }
             fY[r] = ld4(a.yobs + (size_t)b * a.y_cs + (size_t)c * HW + (size_t)gi[r] * L + gj0);
             fM[r] = *reinterpret_cast<const uint32_t*>(a.mask + (size_t)b * a.m_cs + (size_t)gi[r] * L + gj0);
@@ -119,20 +99,6 @@ __device__ __forceinline__ bool sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
         // independent of the row pitch
         normal_quad(a.seed, (uint32_t)(a.chain0 + b), (uint32_t)step, TAG_LANGEVIN,
                     noise_quad((size_t)c * H + (rv[r] ? gi[r] : 0), gj0, W), Zn[r]);
-    }
-    if (MS) {
-        wait_vm0();                                    // the state's sc1 loads landed
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (rv[r] && colok) {
-                fX[r] = tie4(sX[r]);
-                if (!fresh) {
-                    fU0[r] = tie4(sU0[r]);
-                    fU1[r] = tie4(sU1[r]);
-                    if (!ALPHA1) fXS[r] = tie4(sXS[r]);
-                }
-            }
-        }
     }
     // ---- 3. data term Y = (X + c1 g) + c2 Z, TV start state
 #pragma unroll
@@ -173,13 +139,8 @@ __device__ __forceinline__ bool sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
         for (int r = 0; r < R; ++r) {
             if (rv[r] && core[r]) {
                 const size_t base = poff + (size_t)gi[r] * L + gjc;
-                if (MS) {
-                    glds16_sc1(a.mean[par_in] + base, &sh.mst[gi[r] - r0][0][0]);
-                    glds16_sc1(a.sq[par_in] + base, &sh.mst[gi[r] - r0][1][0]);
-                } else {
-                    glds16(a.mean[par_in] + base, &sh.mst[gi[r] - r0][0][0]);
-                    glds16(a.sq[par_in] + base, &sh.mst[gi[r] - r0][1][0]);
-                }
+                glds16(a.mean[par_in] + base, &sh.mst[gi[r] - r0][0][0]);
+                glds16(a.sq[par_in] + base, &sh.mst[gi[r] - r0][1][0]);
             }
         }
     }
@@ -304,10 +265,7 @@ __device__ __forceinline__ bool sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
             if ((lane & 15) == 0) sh.red[it][w][lane >> 4] = rs;
         }
         __syncthreads();
-        if (LAST && EARLY_X) {
-            if (MS) { ok = commit(); decided = true; }
-            if (ok) store_x_side();
-        }
+        if (LAST && EARLY_X) store_x_side();
         // dual: u = prox_sigma_g_conj(u2 + sigma nabla z, ths); u2 += rho (u - u2)
         const float4 dn = (w < NW - 1) ? sh.zrow[w + 1][lane] : zero4;
 #pragma unroll
@@ -348,8 +306,6 @@ __device__ __forceinline__ bool sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
     };
     for (int it = 0; it < n_it - 1; ++it) iteration(it, std::false_type{});
     if (n_it > 0) iteration(n_it - 1, std::true_type{});
-    if (MS && !decided) ok = commit();
-    if (!ok) return false;
     // ---- 5. rel_err partial sums -> the chain's norms (one fp64 atomic per iteration and workgroup)
     if (track) {
         // (on wave 0, before the u2 stores: spreading the sums over waves delays every wave's u2 stores -- 8
@@ -362,9 +318,8 @@ __device__ __forceinline__ bool sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
                 for (int q = 0; q < 4; ++q) { sd += sh.red[t][ww][q].x; sn += sh.red[t][ww][q].y; }
             if (!EXACT) sd *= (double)(a.rho * a.rho);     // fast sums hold (x - x2_prev)^2
             // workgroup x adds to copy x % norm_copies (x & 7 = its XCD when there are 8): fewer adds queue
-            // on one address when many tiles share a chain; MS: the step's parity's copy of ms_norms
-            double* const nc = MS ? a.ms_norms + (size_t)(step & 1) * ((size_t)a.B * a.n_tv * 2)
-                                  : nrm + (size_t)(blockIdx.x % a.norm_copies) * ((size_t)a.B * a.n_tv * 2);
+            // on one address when many tiles share a chain
+            double* const nc = nrm + (size_t)(blockIdx.x % a.norm_copies) * ((size_t)a.B * a.n_tv * 2);
             atomicAdd(&nc[((size_t)b * a.n_tv + t) * 2], sd);
             atomicAdd(&nc[((size_t)b * a.n_tv + t) * 2 + 1], sn);
         }
@@ -404,7 +359,6 @@ __device__ __forceinline__ bool sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
             if (lo ? corelane_o : corelane) st_tile(lo ? pb : pa, v2);
         }
     }
-    return true;
 }
 
 template <bool EXACT, bool ALPHA1, int R, bool GEN, int NW>
@@ -452,8 +406,8 @@ __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
             const int plane = item / T, t = item - plane * T;
             const int seg = GEN ? t / a.nbands : 0;
             const int band = t - seg * a.nbands;
-            if constexpr (SPLIT) sb_tile<EXACT, ALPHA1, R, GEN, NW>(a, sh, plane, seg, band, a.n_tv, true, step, fresh, arrive, no_commit);
-            else sb_tile<EXACT, ALPHA1, R, GEN, NW>(a, sh, plane, seg, band, a.n_tv, true, step, fresh, [] {}, no_commit);
+            if constexpr (SPLIT) sb_tile<EXACT, ALPHA1, R, GEN, NW>(a, sh, plane, seg, band, a.n_tv, true, step, fresh, arrive);
+            else sb_tile<EXACT, ALPHA1, R, GEN, NW>(a, sh, plane, seg, band, a.n_tv, true, step, fresh, [] {});
         }
         if (!SPLIT || item >= N) arrive();
     }
@@ -538,7 +492,7 @@ __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
             const int band = t - seg * a.nbands;
             const int nstop = __builtin_amdgcn_readfirstlane(sh.s_stop[plane / a.C]);
             if (nstop < a.n_tv) {
-                sb_tile<EXACT, ALPHA1, R, GEN, NW>(a, sh, plane, seg, band, nstop, false, step, fresh, [] {}, no_commit);
+                sb_tile<EXACT, ALPHA1, R, GEN, NW>(a, sh, plane, seg, band, nstop, false, step, fresh, [] {});
                 wait_vm0();
                 __syncthreads();
             }
@@ -556,200 +510,6 @@ __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
         if (a.fresh_dev) *a.fresh_dev = 0;
         if (a.advance_step && a.d_step) *a.d_step = step - a.step_offset + 1;   // the value read at the start: no dependent load
     }
-}
-
-// ---------------------------------------------------------------------------------------
-// Multi-step tile kernel (tv_tile_ms_kernel): a.ms_steps consecutive Langevin steps in ONE launch, every tile a
-// workgroup for the whole launch (grid = tiles <= CUs, all resident).  Between steps a tile waits only for the
-// tiles whose core rows / columns its halo reads (per-tile progress words, prog[tile] = steps stored), not for
-// the grid: no launch gap, no grid-wide arrival, no finalising workgroup per step.
-// deepinv's early stop couples a chain's tiles (one rel-err norm per chain and inner iteration): each tile adds
-// its sums of step s to ms_norms[step & 1] and counts itself in cnt[step & 1][chain]; the chain's last tile tests the
-// stop and publishes dec[chain] = (s + 1) << 8 | inner iterations.  With one step of slack: a tile computes step s
-// before dec(s - 1) is known, and waits for it only at its first store of step s (sb_tile's commit hook); the
-// ping-pong state still holds step s - 1's inputs then.  If step s - 1 stopped (rare), every tile of the chain
-// drops step s, redoes step s - 1 with the stopped iteration count, meets the chain's other tiles (rdo[chain]),
-// and computes step s again.  The launch's last step is decided (and redone if it stopped) before the tiles leave;
-// the last workgroup to leave resets the state and advances the step counter by ms_steps.
-// State (a.ms, ints): [0] launch arrivals, dec[B] at 4, cnt[2][B] at 4 + B, rdo[B] at 4 + 3 B, prog[tiles] at
-// 4 + 4 B; a.ms_norms: [2][B][n_tv][2] doubles.  All zero between launches.  Every spin is bounded (guard:
-// arrive[3], FusedTvChains.check_handoff).
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ int poll_sc1(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-// lane 0: spin until *p >= target (bounded); false if the guard expired
-__device__ __forceinline__ bool spin_ge(const int* p, int target, int* guard) {
-    for (int spin = 0; spin < (1 << 22); ++spin) {
-        if (poll_sc1(p) >= target) return true;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    __hip_atomic_store(guard, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return false;
-}
-
-template <bool EXACT, bool ALPHA1, int R, bool GEN>
-__global__ void __launch_bounds__(16 * WAVE) tv_tile_ms_kernel(const TvArgs a) {
-    constexpr int NW = 16;
-    __shared__ TileShared<R, NW> sh;
-    __shared__ int s_ok, s_nstop, s_last;
-    const long long step0 = launch_step(a);
-    const bool fresh0 = launch_fresh(a);
-    const int B = a.B, P = B * a.C;
-    const int T = a.nbands * (GEN ? a.st_nsegs : 1);
-    const int N = P * T, q8 = N >> 3, r8 = N & 7;
-    const int x = blockIdx.x, xcd = x & 7, k8 = x >> 3;
-    const int item = xcd * q8 + min(xcd, r8) + k8;
-    const int plane = item / T, t = item - plane * T;
-    const int seg = GEN ? t / a.nbands : 0;
-    const int band = t - seg * a.nbands;
-    const int ch = plane / a.C;
-    const int Tc = a.C * T;                           // tiles of one chain
-    int* const ms = a.ms;
-    int* const dec = ms + 4;
-    int* const cnt = ms + 4 + B;
-    int* const rdo = ms + 4 + 3 * B;
-    int* const prog = ms + 4 + 4 * B;
-    int* const guard = a.arrive + 3;
-    // the tiles whose core rows / columns this tile's halo reads: bands covering rows [e0, e1), column segments
-    // covering the window [f0, f0 + 256)
-    const int H = a.H, h = a.halo;
-    const int r0 = band * a.band_h, r1 = min(H, r0 + a.band_h);
-    const int e0 = max(0, r0 - h), e1 = min(H, r1 + h);
-    const int b_lo = e0 / a.band_h, b_hi = min(a.nbands - 1, (e1 - 1) / a.band_h);
-    int s_lo = 0, s_hi = 0;
-    if (GEN) {
-        const int cc0 = seg * a.st_seg_w;
-        const int f0 = max(0, cc0 - a.st_halo) & ~3;
-        const int fend = min(a.W, f0 + TV_COLS);
-        s_lo = min(a.st_nsegs - 1, f0 / a.st_seg_w);
-        s_hi = min(a.st_nsegs - 1, (fend - 1) / a.st_seg_w);
-    }
-    // One tile call site (a second inlined copy of the tile pass spills at 48-row tiles): step s, or -- redoing --
-    // step s - 1 with the stopped iteration count (then the chain's barrier); s == ms_steps: the last step's
-    // decision, and its redo if it stopped.
-    int handled = -1;                                 // step whose predecessor's stop was already redone
-    int rounds = 0;                                   // chain barriers passed (redos)
-    bool redoing = false;
-    for (int s = 0;;) {
-        if (s == a.ms_steps && !redoing) {
-            if (threadIdx.x == 0) {
-                spin_ge(dec + ch, s << 8, guard);
-                s_nstop = poll_sc1(dec + ch) & 0xFF;
-            }
-            __syncthreads();
-            if (s_nstop >= a.n_tv) break;
-            redoing = true;
-        }
-        // this tile's inputs: the halo neighbours' step s - 1 outputs stored
-        if (!redoing && s > 0) {
-            if (threadIdx.x == 0) {
-                for (int bb = b_lo; bb <= b_hi; ++bb)
-                    for (int sg = s_lo; sg <= s_hi; ++sg) {
-                        const int it = plane * T + sg * a.nbands + bb;
-                        if (it != item) spin_ge(prog + it, s, guard);
-                    }
-            }
-            __syncthreads();
-        }
-        // commit: step s - 1's stop decision (published by its chain's last tile), once per step
-        auto commit = [&]() -> bool {
-            if (redoing || s == 0 || handled == s) return true;
-            if (threadIdx.x == 0) {
-                spin_ge(dec + ch, s << 8, guard);    // dec = (s' + 1) << 8 | n for the latest decided step s'
-                const int d = poll_sc1(dec + ch);
-                s_nstop = d & 0xFF;
-                s_ok = s_nstop >= a.n_tv ? 1 : 0;
-            }
-            __syncthreads();
-            return s_ok != 0;
-        };
-        const int ss = redoing ? s - 1 : s;
-        const bool ok = sb_tile<EXACT, ALPHA1, R, GEN, NW, true>(a, sh, plane, seg, band, redoing ? s_nstop : a.n_tv,
-                                                                 !redoing, step0 + ss, fresh0 && ss == 0, [] {}, commit);
-        if (redoing) {                                // step s - 1 redone: meet the chain's other tiles
-            ++rounds;
-            wait_vm0();
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                __hip_atomic_fetch_add(rdo + ch, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                spin_ge(rdo + ch, rounds * Tc, guard);
-            }
-            __syncthreads();
-            redoing = false;
-            if (s == a.ms_steps) break;
-            handled = s;
-            continue;                                 // step s again, from the redone state
-        }
-        if (!ok) {                                    // rare: the chain stopped at step s - 1
-            redoing = true;
-            continue;
-        }
-        // this tile's rel-err sums of step s are added (sb_tile: to ms_norms[(step0 + s) & 1]): count them; the
-        // chain's last tile decides step s
-        const int par = (int)((step0 + s) & 1);
-        wait_vm0();
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const int old = __hip_atomic_fetch_add(cnt + par * B + ch, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_last = old == Tc - 1 ? 1 : 0;
-            s_nstop = 0;
-        }
-        __syncthreads();
-        if (s_last) {
-            const int tt = threadIdx.x;
-            if (tt >= trk_lo(a) && tt <= trk_hi(a) && tt < a.n_tv) {
-                double* const n0 = a.ms_norms + (size_t)par * ((size_t)B * a.n_tv * 2) + ((size_t)ch * a.n_tv + tt) * 2;
-                const double nd = __hip_atomic_exchange(n0, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const double nn = __hip_atomic_exchange(n0 + 1, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const float rel = (float)sqrt(nd) / (float)sqrt(nn);
-                if (rel < a.tol) atomicOr(&s_nstop, 1 << tt);
-            }
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                const int m = s_nstop;
-                const int n = m ? (__ffs(m) - 1) + 1 : a.n_tv;
-                __hip_atomic_store(cnt + par * B + ch, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(dec + ch, ((s + 1) << 8) | n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        // progress: this tile's step-s outputs (sc1 stores) drained
-        wait_vm0();
-        __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_store(prog + item, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ++s;
-    }
-    // leave: the last workgroup resets the launch state and advances the step counter
-    wait_vm0();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int old = __hip_atomic_fetch_add(ms, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = old == (int)gridDim.x - 1 ? 1 : 0;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    for (int i = threadIdx.x; i < N; i += blockDim.x) __hip_atomic_store(prog + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int i = threadIdx.x; i < B; i += blockDim.x) {
-        __hip_atomic_store(dec + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(rdo + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (threadIdx.x == 0) {
-        __hip_atomic_store(ms, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (a.fresh_dev) *a.fresh_dev = 0;
-        if (a.advance_step && a.d_step) *a.d_step = step0 - a.step_offset + a.ms_steps;
-    }
-}
-
-bool launch_tile_ms(const TvArgs& s, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen) {
-#define PSGLA_TILE(E, A, RV) \
-    if (exact == E && alpha1 == A && s.tile_nw == 16 && s.tile_r == RV) { \
-        if (!gen) hipLaunchKernelGGL((tv_tile_ms_kernel<E, A, RV, false>), grid, dim3(16 * WAVE), 0, st, s); \
-        else hipLaunchKernelGGL((tv_tile_ms_kernel<E, A, RV, true>), grid, dim3(16 * WAVE), 0, st, s);      \
-        return true; \
-    }
-#define PSGLA_TILES(E, A) PSGLA_TILE(E, A, 2) PSGLA_TILE(E, A, 3)
-    PSGLA_TILES(true, true) PSGLA_TILES(true, false) PSGLA_TILES(false, true) PSGLA_TILES(false, false)
-#undef PSGLA_TILES
-#undef PSGLA_TILE
-    return false;
 }
 
 bool launch_tile(const TvArgs& s, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen) {

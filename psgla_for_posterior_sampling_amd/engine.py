@@ -29,8 +29,7 @@ class FusedTvChains:
                  n_inter: int, n_inter_mmse: int, chain0: int = 0, exact: bool = False,
                  tv_x2: torch.Tensor | None = None, tv_u2: torch.Tensor | None = None,
                  store_samples: bool = True, store_blocks: bool = True, kernel_variant: str = "auto",
-                 stream_wgs: int = 0, stream_windows: str = "auto", parallel_redo: bool = True,
-                 tile_multi_steps: int = 0):
+                 stream_wgs: int = 0, stream_windows: str = "auto", parallel_redo: bool = True):
         if init.dim() != 4:
             raise ValueError("init must be (B, C, H, W)")
         if tv.n_it > N.TV_MAX_FUSED_IT:
@@ -108,20 +107,6 @@ class FusedTvChains:
         d.redo = self.work.redo.data_ptr() if parallel_redo else None
         self.desc = d
         self._unsettled = False
-        # multi-step tile launches (tv_tile_ms_kernel): graph segments run as launches of `tile_multi_steps` steps
-        # each where the library takes them (psgla_tv_step_kernel() == 5); eager steps stay one per launch
-        self.desc_ms = None
-        self.multi_steps = 0
-        if int(tile_multi_steps) > 1:
-            self.ms_state = torch.zeros(4 + 4 * B + 4096, dtype=torch.int32, device=dev)
-            self.ms_norms = torch.zeros((2, B, max(tv.n_it, 1), 2), dtype=torch.float64, device=dev)
-            dm = N.PsglaTvStep.from_buffer_copy(d)
-            dm.multi_steps = int(tile_multi_steps)
-            dm.ms_state = self.ms_state.data_ptr()
-            dm.ms_norms = self.ms_norms.data_ptr()
-            if N.lib().psgla_tv_step_kernel(ctypes.byref(dm)) == 5:
-                self.desc_ms = dm
-                self.multi_steps = int(tile_multi_steps)
         self.sched_struct = self.sched.struct(True, 0)
         if self.warm_first:
             # first step of a warm-started run: the TV primal x2 (previous run's state) is not X
@@ -186,14 +171,9 @@ class FusedTvChains:
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
-        ms = self.multi_steps if (self.multi_steps and steps_per_graph % self.multi_steps == 0) else 0
         with torch.cuda.graph(g, stream=s):
-            if ms:
-                for _ in range(steps_per_graph // ms):
-                    self._launch(self.desc_ms)
-            else:
-                for _ in range(steps_per_graph):
-                    self._launch(self.desc)
+            for _ in range(steps_per_graph):
+                self._launch(self.desc)
         torch.cuda.current_stream().wait_stream(s)
         self.graph = g
         self.graph_steps = steps_per_graph
@@ -255,13 +235,6 @@ class FusedTvChains:
         if k < 0:
             raise RuntimeError(N.lib().psgla_last_error().decode())
         return {0: "tv_main_kernel", 1: "tv_stream_kernel", 3: "tv_tile_kernel"}[k]
-
-    @property
-    def graph_kernel(self) -> str:
-        """The kernel the captured graph segments launch (tv_tile_ms_kernel when multi-step launches apply)."""
-        if self.multi_steps and self.graph_steps and self.graph_steps % self.multi_steps == 0:
-            return "tv_tile_ms_kernel"
-        return self.main_kernel
 
     def launch_main_only(self, n: int = 1):
         """Launch only the fused tile kernel n times for the CURRENT step (idempotent: it reads

@@ -990,43 +990,3 @@ def test_parallel_early_stop_redo_equals_serial(B, H, W, variant, stream_wgs):
             outs.append((eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone()))
         for a, b in zip(*outs):
             assert torch.equal(a, b), (tol, B, H, W, variant)
-
-
-@pytest.mark.parametrize("B,H,W,ms,tol", [(8, 256, 256, 10, 1e-5), (8, 256, 256, 5, 3e-3), (8, 256, 256, 10, 0.2),
-                                          (1, 481, 321, 10, 1e-5), (1, 481, 321, 5, 3e-3), (2, 321, 481, 5, 0.2),
-                                          (2, 256, 256, 10, 3e-3)])
-def test_tile_multi_step_equals_single_step(B, H, W, ms, tol):
-    """tv_tile_ms_kernel (ABI 11: `ms` steps per launch, tiles synchronised only with their halo neighbours,
-    deepinv's per-chain stop taken with one step of slack and redone in place) gives chains bit-identical to one
-    tv_tile_kernel launch per step, in both arithmetic modes: the bench's 8 chains (48-row tiles), castle at batch 1
-    and CBSD68's 321 x 481 at batch 2 (32-row tiles, column segments, padded rows), at tolerances where the stop
-    never / sometimes / always fires."""
-    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
-    from psgla_for_posterior_sampling_amd import hip_ops as K
-    g = torch.Generator(device=DEV).manual_seed(31)
-    xs = torch.rand((B, 3, H, W), generator=g, device=DEV)
-    gen = torch.Generator(device=DEV).manual_seed(0)
-    mask2d = (torch.rand((H, W), generator=gen, device=DEV) > 0.5).to(torch.uint8)
-    y = mask2d.float() * xs + torch.normal(torch.zeros_like(xs), std=(1 / 255.0) * torch.ones_like(xs), generator=gen)
-    init = (mask2d.float() * y + (1 - mask2d.float()) * 0.5).contiguous()
-    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
-    for exact in (True, False):
-        outs = []
-        for multi in (0, ms):
-            eng = FusedTvChains(init, y.contiguous(), mask2d, c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
-                                alpha=1.0, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10, tol=tol),
-                                seed=2, n_iter=31, n_inter=3, n_inter_mmse=4, exact=exact, kernel_variant="tile",
-                                tile_multi_steps=multi)
-            assert eng.main_kernel == "tv_tile_kernel"
-            assert eng.multi_steps == multi
-            eng.run(31, graph_steps=10)           # 3 graph segments, then one eager step
-            torch.cuda.synchronize()
-            if multi:
-                assert eng.graph_kernel == "tv_tile_ms_kernel"
-                assert not torch.any(eng.ms_state != 0).item(), "multi-step state not reset"
-                assert not torch.any(eng.ms_norms != 0).item(), "multi-step rel-err sums not reset"
-            eng.check_handoff()
-            bm, bm2 = eng.blocks()
-            outs.append((eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone()))
-        for a, b in zip(*outs):
-            assert torch.equal(a, b), (exact, B, H, W, ms, tol)
