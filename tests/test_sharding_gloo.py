@@ -110,16 +110,20 @@ def _fake_record(i):
 N_IMAGES = 5
 
 
-def _records_worker(rank, world, port, out_dir):
+def _records_worker(rank, world, port, out_dir, backend="gloo"):
     from psgla_for_posterior_sampling_amd.sharding import gather_records, reduce_dataset_psnr
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = "cpu"
+    if backend == "nccl":                    # one GPU per rank (RCCL refuses two ranks on one device)
+        torch.cuda.set_device(rank)
+        dev = f"cuda:{rank}"
+    dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         a, b = chain_range(N_IMAGES, world, rank)
         local = {i: _fake_record(i) for i in range(a, b)}
-        s, q, n = reduce_dataset_psnr(local, world, "cpu")
-        got = gather_records(local, world, rank, "cpu")
+        s, q, n = reduce_dataset_psnr(local, world, dev)
+        got = gather_records(local, world, rank, dev)
         torch.save({"sum": s, "n": n, "none": got is None}, os.path.join(out_dir, f"s{rank}.pt"))
         if rank == 0:
             import pickle
@@ -129,15 +133,12 @@ def _records_worker(rank, world, port, out_dir):
         dist.destroy_process_group()
 
 
-def test_two_rank_records_gather_exact(tmp_path):
-    """The sharded CLI's result path (sampling_images.main, world > 1): per-image records gathered to rank 0
-    through one float64 tensor per rank plus gather_object metadata -- every array, list, scalar, dtype and
-    the mask come back identical; the dataset PSNR all_reduce counts every image once; other ranks get None."""
+def _check_records_gather(tmp_path, backend):
     import pickle
     import numpy as np
     world = 2
-    mp.start_processes(_records_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
-                       start_method="spawn")
+    mp.start_processes(_records_worker, args=(world, _free_port(), str(tmp_path), backend), nprocs=world,
+                       join=True, start_method="spawn")
     with open(os.path.join(tmp_path, "records.pkl"), "rb") as f:
         got = pickle.load(f)
     assert sorted(got) == list(range(N_IMAGES))
@@ -156,3 +157,19 @@ def test_two_rank_records_gather_exact(tmp_path):
         assert s["n"] == N_IMAGES
         assert abs(s["sum"] - sum(27.0 + i for i in range(N_IMAGES))) < 1e-9
         assert s["none"] == (r != 0)
+
+
+def test_two_rank_records_gather_exact(tmp_path):
+    """The sharded CLI's result path (sampling_images.main, world > 1): per-image records gathered to rank 0
+    through one float64 tensor per rank plus gather_object metadata -- every array, list, scalar, dtype and
+    the mask come back identical; the dataset PSNR all_reduce counts every image once; other ranks get None."""
+    _check_records_gather(tmp_path, "gloo")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2,
+                    reason="the RCCL path needs two GPUs (one rank per device)")
+def test_two_rank_records_gather_exact_nccl(tmp_path):
+    """The same gather over RCCL (dist_backend's choice on a multi-GPU node): the float64 transport tensors
+    live on each rank's device."""
+    _check_records_gather(tmp_path, "nccl")
