@@ -186,15 +186,21 @@ class FusedTvChains:
             self.steps_done += self.graph_steps
             self._unsettled = True
 
-    def rewind(self, step: int):
+    def rewind(self, step: int, discard_pending: bool = False):
         """Set the step index (device counter, stream-ordered, and host count) back to `step`, which
         must have the parity of the current step (the ping-pong state stays where it is).  For
         benchmarking only: untimed warm-up replays can then run for any length of time and the timed
-        steps still write the sample / block slots of the schedule (the chain state simply continues)."""
+        steps still write the sample / block slots of the schedule (the chain state simply continues).
+        discard_pending: drop a pending early-stop redo instead of settling it (warm-up replays whose state
+        restore() undoes: no redo-only launch per replay in a kernel trace)."""
         step = int(step)
         if step < 0 or (step - self.steps_done) % 2:
             raise ValueError("rewind target must be >= 0 and of the current step's parity")
-        self.settle()                     # a pending redo belongs to the step before the rewind
+        if discard_pending:
+            self.work.redo.zero_()
+            self._unsettled = False
+        else:
+            self.settle()                 # a pending redo belongs to the step before the rewind
         self.sched.d_step.fill_(step)
         self.steps_done = step
 
