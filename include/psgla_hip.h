@@ -85,13 +85,13 @@ typedef struct PsglaSchedule {
  *     band kernel (tv_main_kernel) followed by a small finaliser kernel
  *     (tv_finalise_kernel, <= 8 workgroups) that does the same.
  * launch_mask 1 launches only the main pass of either variant (timing).
- * deepinv's early stop (rare at the reference's settings) in the row stream with a `redo` buffer (ABI 11) and a
- * grid the CUs hold at once: the step's finaliser only records which chains stopped (redo[4 + g] = their
- * inner-iteration count, redo[0] = pending); the NEXT launch's workgroups first redo the stopped chains' part of
- * that step -- every workgroup its own rows, all in parallel --, meet at one grid barrier (redo[1]), then run their
- * own step.  A run's last step is settled by launch_mask 4 (the pending redo alone, then redo[0] cleared), which
- * the host issues before it reads results.  Without `redo` (or with a larger grid), and in the tile kernel, the
- * finaliser's workgroup recomputes the stopped chains itself, one (plane, segment) / tile after another.
+ * deepinv's early stop (rare at the reference's settings) in the row stream and the tile kernel with a `redo`
+ * buffer (ABI 11) and a grid the CUs hold at once: the step's finaliser only records which chains stopped
+ * (redo[4 + g] = their inner-iteration count, redo[0] = pending); the NEXT launch's workgroups first redo the
+ * stopped chains' part of that step -- every workgroup its own rows / tile, all in parallel --, meet at one grid
+ * barrier (redo[1]), then run their own step.  A run's last step is settled by launch_mask 4 (the pending redo
+ * alone, then redo[0] cleared), which the host issues before it reads results.  Without `redo` (or with a larger
+ * grid), the finaliser's workgroup recomputes the stopped chains itself, one (plane, segment) / tile after another.
  * ------------------------------------------------------------------------------- */
 typedef struct PsglaTvStep {
     int32_t B, C, H, W;

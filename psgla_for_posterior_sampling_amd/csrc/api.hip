@@ -134,7 +134,12 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
         s.redo_only = 1;
         int rc;
         if (a.tile_r > 0) {
-            return 0;                    // (the tile kernel's finaliser recomputes stopped chains itself)
+            const int grid = P * s.nbands * s.st_nsegs;
+            s.par_redo = grid <= device_cus() ? 1 : 0;
+            if (!s.par_redo) return 0;   // (the tile kernel's finaliser recomputed stopped chains itself)
+            if (!launch_tile(s, dim3(grid), st, EXACT, ALPHA1, !(s.ldw == s.W && s.st_nsegs == 1)))
+                return fail(0, "psgla_tv_step: internal error: no tile kernel of this shape");
+            rc = launch_check("tv_tile_kernel(redo)");
         } else {
             const int grid = s.split_wgs > 0 ? s.split_wgs : s.st_nvp;
             s.par_redo = grid <= device_cus() ? 1 : 0;
@@ -157,7 +162,9 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
             // reads issued back to back (round 4), 8 copies cost 8 chains of 30 tiles +1.6 % and save castle at
             // batch 2 (108 tiles per chain) 3.5 % and at batch 1 (246) 5 % (profiles/r04k_tile_fin_ab.txt)
             if (s.norm_copies < 1 || s.C * s.nbands * s.st_nsegs < 64) s.norm_copies = 1;
-            s.par_redo = 0;              // the tile kernel recomputes stopped chains in its finalising workgroup
+            // parallel early-stop redo when every tile is resident at once (its grid barrier); otherwise the
+            // finalising workgroup recomputes stopped chains itself
+            s.par_redo = (s.redo && grid <= device_cus()) ? 1 : 0;
             const bool gen = !(s.ldw == s.W && s.st_nsegs == 1);
             if (launch_tile(s, dim3(grid), st, EXACT, ALPHA1, gen)) return launch_check("tv_tile_kernel");
             return fail(0, "psgla_tv_step: internal error: no tile kernel of this shape");

@@ -263,6 +263,14 @@ __device__ __forceinline__ void glds16(const void* src, void* dst) {
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
                  :: "v"(src), "s"(off) : "memory", "m0");
 }
+// glds16 at base + byte_off for a base whose LDS address folds to a constant (a __shared__ array) and a
+// wave-uniform offset, forced into a scalar register: a call site the compiler cannot prove uniform (the tile
+// kernel's second, early-stop redo, instance of its tile) otherwise leaves the m0 operand in a VGPR
+__device__ __forceinline__ void glds16_at(const void* src, void* base, int byte_off) {
+    const unsigned off = (unsigned)(size_t)(lptr_t)base + (unsigned)__builtin_amdgcn_readfirstlane(byte_off);
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :: "v"(src), "s"(off) : "memory", "m0");
+}
 __device__ __forceinline__ void glds4(const void* src, void* dst) {
     const unsigned off = (unsigned)(size_t)(lptr_t)dst;
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off"

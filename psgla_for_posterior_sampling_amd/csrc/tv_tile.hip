@@ -139,8 +139,9 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
         for (int r = 0; r < R; ++r) {
             if (rv[r] && core[r]) {
                 const size_t base = poff + (size_t)gi[r] * L + gjc;
-                glds16(a.mean[par_in] + base, &sh.mst[gi[r] - r0][0][0]);
-                glds16(a.sq[par_in] + base, &sh.mst[gi[r] - r0][1][0]);
+                const int ro = (gi[r] - r0) * (int)sizeof(sh.mst[0]);
+                glds16_at(a.mean[par_in] + base, &sh.mst[0][0][0], ro);
+                glds16_at(a.sq[par_in] + base, &sh.mst[0][1][0], ro);
             }
         }
     }
@@ -378,6 +379,26 @@ __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
         const int N = P * T, q8 = N >> 3, r8 = N & 7;
         const int x = blockIdx.x, xcd = x & 7, k = x >> 3;
         const int item = xcd * q8 + min(xcd, r8) + k;
+        // The previous step's pending early-stop redo (rare; a.redo[0], published by that step's finaliser; round 5):
+        // every workgroup whose chain stopped redoes its own tile of that step with the stopped iteration count
+        // (the step's inputs are intact: ping-pong state), all in parallel, then one grid barrier before this
+        // step reads them.  launch_mask 4 (redo_only): the redo alone.
+        if (a.par_redo && (a.fin_inline || a.redo_only)) {
+            const int pend = __builtin_amdgcn_readfirstlane(a.redo[0]);
+            if (pend & 1) {
+                if (item < N) {
+                    const int plane = item / T, t = item - plane * T;
+                    const int seg = GEN ? t / a.nbands : 0;
+                    const int band = t - seg * a.nbands;
+                    const int nstop = __builtin_amdgcn_readfirstlane(a.redo[4 + plane / a.C]);
+                    if (nstop < a.n_tv)
+                        sb_tile<EXACT, ALPHA1, R, GEN, NW>(a, sh, plane, seg, band, nstop, false, step - 1,
+                                                           (pend & 2) != 0, [] {});
+                }
+                if (!a.redo_only) grid_sync(a.redo + 1, a.arrive + 3);
+            }
+            if (a.redo_only) return;
+        }
         // Arrival.  The 72-row tiles (SPLIT) arrive before their u2 stores, so those drain while the last
         // workgroup finalises (16 chains 68.3 -> 67.0 us; the 16-wave tiles measured +1-1.4 % that way,
         // profiles/r03s_tile_two_phase_ab.txt): the counter a.arrive then holds two counts, the low 16 bits
@@ -470,7 +491,15 @@ __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
         if (m) sh.s_item = 1;
     }
     __syncthreads();
-    if (sh.s_item) {
+    if (a.par_redo) {
+        // parallel redo (next launch, or launch_mask 4): publish the stop counts and the pending flag, reset the
+        // grid-barrier count (every workgroup of this launch passed it before its tile)
+        for (int g = threadIdx.x; g < G; g += blockDim.x) a.redo[4 + g] = sh.s_stop[g];
+        if (threadIdx.x == 0) {
+            a.redo[1] = 0;
+            a.redo[0] = sh.s_item ? (1 | (fresh ? 2 : 0)) : 0;
+        }
+    } else if (sh.s_item) {
         // rare: redo every tile of a stopped chain with the stopped iteration count (inputs intact), once every
         // other workgroup's stores are complete (phase 2; all of them have arrived, so each will count: bounded
         // wait only as a guard)

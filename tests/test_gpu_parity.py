@@ -955,15 +955,16 @@ def test_tile_kernel_early_stop_handoff_full_size(B, H, W, tol):
 
 @pytest.mark.parametrize("B,H,W,variant,stream_wgs", [(64, 256, 256, "stream", 0), (64, 481, 321, "stream", 0),
                                                        (6, 40, 52, "stream", -1), (8, 256, 256, "tile", 0),
-                                                       (1, 481, 321, "tile", 0)])
+                                                       (1, 481, 321, "tile", 0), (24, 130, 64, "tile", 0)])
 def test_parallel_early_stop_redo_equals_serial(B, H, W, variant, stream_wgs):
-    """ABI 11: when deepinv's early stop fires in the row stream, the next launch's workgroups redo the stopped
-    chains' part of the step in parallel (each its own rows, then a grid barrier), the run's last step through
-    launch_mask 4; the finaliser's serial recompute (no redo buffer) is the reference.  (The tile kernel keeps the
-    serial recompute with or without the buffer: its cases check that the buffer changes nothing there.)  tol = 0.2 makes the stop fire on every
+    """ABI 11: when deepinv's early stop fires in the row stream or the tile kernel, the next launch's workgroups
+    redo the stopped chains' part of the step in parallel (each its own rows / tile, then a grid barrier), the
+    run's last step through launch_mask 4; the finaliser's serial recompute (no redo buffer) is the reference.
+    tol = 0.2 makes the stop fire on every
     chain in every step (after 3 inner iterations), tol = 2e-3 on some steps only; fast kernels, hipGraph replay,
     the bench shape (64 chains: row split, 256 workgroups), the castle shape at 64 chains (half-wave windows,
-    segments), per-plane streams, the 8-chain tile kernel and castle at batch 1: bit-identical."""
+    segments), per-plane streams, the 8-chain tile kernel, castle at batch 1 and 72-row tiles of 8 waves (two-phase
+    arrival): bit-identical."""
     from psgla_for_posterior_sampling_amd.engine import FusedTvChains
     from psgla_for_posterior_sampling_amd import hip_ops as K
     g = torch.Generator(device=DEV).manual_seed(5)
