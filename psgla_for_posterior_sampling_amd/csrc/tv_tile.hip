@@ -215,12 +215,13 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
         const float4 up = (w > 0) ? sh.urow[w - 1][lane] : zero4;
         // the wave's first row -- the only one reading the hand-off from the wave above -- last, so that LDS
         // read's latency hides behind the other rows (-0.9 % at 8 chains, profiles/r03o_tile_row0_last_ab.txt)
+        if (act_p) {
 #pragma unroll
         for (int rr = 0; rr < R; ++rr) {
             const int r = (rr + 1) % R;
-            if (!act_p) break;
             const float u1l = __int_as_float(
                 __builtin_amdgcn_update_dpp(0, __float_as_int(u1[r][CPL - 1]), 0x138 /* wave_shr:1 */, 0xF, 0xF, true));
+            float rd = 0.f, rn = 0.f;                      // fast: the row's rel-err terms (as the row stream)
 #pragma unroll
             for (int k = 0; k < CPL; ++k) {
                 // the row above: 0 above the tile's first row (the plane's top row or an artificial halo edge)
@@ -239,24 +240,31 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
                     xn = __builtin_fmaf(a.rho, xv - xo, xo);
                 }
                 // rel-err terms of the counted rows (row-uniform test; lanes past W are masked once, at
-                // the reduction: adding nothing and adding +0 leave a lane's sum identical)
-                if (trk && core[r] && rv[r]) {
-                    const bool real = !GEN || k < nreal;   // padding columns are not part of the norms
-                    if (EXACT) {
+                // the reduction: adding nothing and adding +0 leave a lane's sum identical).  Fast mode (round 5):
+                // every row's terms into its own partial sums, added once per row -- a per-element select of the
+                // running sums cost 2 VALU per element (the row stream's order)
+                const bool real = !GEN || k < nreal;       // padding columns are not part of the norms
+                if (EXACT) {
+                    if (trk && core[r] && rv[r]) {
                         const float d = real ? xo - xn : 0.f;
                         const float q = real ? xn + 1e-12f : 0.f;
                         sd = __builtin_fmaf(d, d, sd);
                         sn = __builtin_fmaf(q, q, sn);
-                    } else {
-                        const float d = real ? xv - xo : 0.f;
-                        const float q = real ? xn : 0.f;
-                        sd = __builtin_fmaf(d, d, sd);
-                        sn = __builtin_fmaf(q, q, sn);
                     }
+                } else if (trk) {
+                    const float d = real ? xv - xo : 0.f;
+                    const float q = real ? xn : 0.f;
+                    rd = __builtin_fmaf(d, d, rd);
+                    rn = __builtin_fmaf(q, q, rn);
                 }
                 z[r][k] = zv;
                 x2[r][k] = xn;
             }
+            if (!EXACT && trk && core[r] && rv[r]) {
+                sd += rd;
+                sn += rn;
+            }
+        }
         }
         if (act_p) sh.zrow[w][lane] = make_float4(z[0][0], z[0][1], z[0][2], z[0][3]);
         if (trk) {
@@ -269,12 +277,15 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
         if (LAST && EARLY_X) store_x_side();
         // dual: u = prox_sigma_g_conj(u2 + sigma nabla z, ths); u2 += rho (u - u2)
         const float4 dn = (w < NW - 1) ? sh.zrow[w + 1][lane] : zero4;
+        if (act_d) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            if (!act_d) break;
             const float zr3 = __int_as_float(
                 __builtin_amdgcn_update_dpp(0, __float_as_int(z[r][0]), 0x130 /* wave_shl:1 */, 0xF, 0xF, true));
             const bool down = gi[r] < H - 1;
+            // fast mode (round 5): the plane's last row (no vertical difference) takes sigma 0 in its dual -- a
+            // row-uniform scalar instead of a per-element select (the same value: sigma * 0 == 0 * finite)
+            const float sg0 = down ? a.sig_tv : 0.f;
 #pragma unroll
             for (int k = 0; k < CPL; ++k) {
                 const float zc = z[r][k];
@@ -293,7 +304,7 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
                     u0[r][k] = uo0 + a.rho * (v0 / dd - uo0);
                     u1[r][k] = uo1 + a.rho * (v1 / dd - uo1);
                 } else {
-                    const float v0 = __builtin_fmaf(a.sig_tv, g0, uo0);
+                    const float v0 = __builtin_fmaf(sg0, zd - zc, uo0);
                     const float v1 = __builtin_fmaf(a.sig_tv, g1, uo1);
                     const float s2 = __builtin_fmaf(v0, v0, v1 * v1);
                     const float f = fminf(1.0f, a.ths * __builtin_amdgcn_rsqf(s2));
@@ -301,6 +312,7 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
                     u1[r][k] = __builtin_fmaf(a.rho, __builtin_fmaf(v1, f, -uo1), uo1);
                 }
             }
+        }
         }
         if (act_d) sh.urow[w][lane] = make_float4(u0[R - 1][0], u0[R - 1][1], u0[R - 1][2], u0[R - 1][3]);
         __syncthreads();
