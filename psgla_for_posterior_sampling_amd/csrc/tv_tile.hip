@@ -148,6 +148,11 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
 
     // ---- 4. inner TV iterations (deepinv 0.2.1 TVDenoiser, the stream kernel's arithmetic)
     const bool lastlane = gj0 + CPL == W;              // holds column W-1: no forward difference there
+    // fast mode (round 5): the horizontal difference's sigma per lane column, 0 at column W-1 -- a per-lane constant
+    // instead of a select per element and iteration (the same value: sigma * finite == 0 there)
+    float sg1[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) sg1[k] = (GEN ? lastk == k : (k == CPL - 1 && lastlane)) ? 0.f : a.sig_tv;
     // Trapezoid: the core rows need iteration j (1-based) only on rows [r0 - (n_it - j), r1 + (n_it - j))
     // for the dual and one row more below for the primal (the dual of a row reads the next row's z);
     // a wave none of whose rows is needed skips the phase (its stale rows feed only unneeded rows).
@@ -305,7 +310,7 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
                     u1[r][k] = uo1 + a.rho * (v1 / dd - uo1);
                 } else {
                     const float v0 = __builtin_fmaf(sg0, zd - zc, uo0);
-                    const float v1 = __builtin_fmaf(a.sig_tv, g1, uo1);
+                    const float v1 = __builtin_fmaf(sg1[k], zr - zc, uo1);
                     const float s2 = __builtin_fmaf(v0, v0, v1 * v1);
                     const float f = fminf(1.0f, a.ths * __builtin_amdgcn_rsqf(s2));
                     u0[r][k] = __builtin_fmaf(a.rho, __builtin_fmaf(v0, f, -uo0), uo0);
