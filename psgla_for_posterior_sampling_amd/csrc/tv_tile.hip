@@ -209,9 +209,12 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
     };
     // one inner iteration; the last one (peeled: LAST is a compile-time constant at both call sites, so
     // the output addressing is not live across the loop) issues the X side between its two phases
-    auto iteration = [&](const int it, auto last_tag) {
+    // TM: whether the iteration's rel-err terms are tracked -- 0 no, 1 yes (compile time: the loops below run the
+    // untracked and tracked iterations as separate straight-line bodies), 2 decided at run time (the peeled last one)
+    auto iteration = [&](const int it, auto last_tag, auto tm_tag) {
         constexpr bool LAST = decltype(last_tag)::value;
-        const bool trk = track && it >= trk_lo(a) && it <= trk_hi(a);
+        constexpr int TM = decltype(tm_tag)::value;
+        const bool trk = TM == 2 ? (track && it >= trk_lo(a) && it <= trk_hi(a)) : TM == 1;
         float sd = 0.f, sn = 0.f;
         const int span = n_it - 1 - it;
         const bool act_p = wr1 > r0 - span && wr0 < r1 + span + 1;
@@ -322,8 +325,19 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
         if (act_d) sh.urow[w][lane] = make_float4(u0[R - 1][0], u0[R - 1][1], u0[R - 1][2], u0[R - 1][3]);
         __syncthreads();
     };
-    for (int it = 0; it < n_it - 1; ++it) iteration(it, std::false_type{});
-    if (n_it > 0) iteration(n_it - 1, std::true_type{});
+    // iterations [0, t0) and [t1, n_it - 1) untracked, [t0, t1) tracked (round 5: one loop with a run-time test
+    // merged both paths and paid register copies for it on every iteration), the last one peeled
+    {
+        using TM0 = std::integral_constant<int, 0>;
+        using TM1 = std::integral_constant<int, 1>;
+        const int nl = max(n_it - 1, 0);
+        const int t0 = track ? min(max(trk_lo(a), 0), nl) : nl;
+        const int t1 = track ? min(max(trk_hi(a) + 1, t0), nl) : nl;
+        for (int it = 0; it < t0; ++it) iteration(it, std::false_type{}, TM0{});
+        for (int it = t0; it < t1; ++it) iteration(it, std::false_type{}, TM1{});
+        for (int it = t1; it < nl; ++it) iteration(it, std::false_type{}, TM0{});
+    }
+    if (n_it > 0) iteration(n_it - 1, std::true_type{}, std::integral_constant<int, 2>{});
     // ---- 5. rel_err partial sums -> the chain's norms (one fp64 atomic per iteration and workgroup)
     if (track) {
         // (on wave 0, before the u2 stores: spreading the sums over waves delays every wave's u2 stores -- 8
