@@ -22,7 +22,8 @@ PATCHES = [
     ("\ntemplate <int R, int NW>\nstruct TileShared {", DEFS, 1),
     ("    // ---- 3. data term Y = (X + c1 g) + c2 Z, TV start state", "    if (track) tdiag(step, 1);\n    // ---- 3. data term Y = (X + c1 g) + c2 Z, TV start state", 1),
     ("    __syncthreads();\n    // The previous mean / sq of the core rows", "    __syncthreads();\n    if (track) tdiag(step, 2);\n    // The previous mean / sq of the core rows", 1),
-    ("    if (n_it > 0) iteration(n_it - 1, std::true_type{});\n", "    if (n_it > 0) iteration(n_it - 1, std::true_type{});\n    if (track) tdiag(step, 3);\n", 1),
+    ("    if (n_it > 0) iteration(n_it - 1, std::true_type{}, std::integral_constant<int, 2>{});\n",
+     "    if (n_it > 0) iteration(n_it - 1, std::true_type{}, std::integral_constant<int, 2>{});\n    if (track) tdiag(step, 3);\n", 1),
     ("            if (lo ? corelane_o : corelane) st_tile(lo ? pb : pa, v2);\n        }\n    }\n",
      "            if (lo ? corelane_o : corelane) st_tile(lo ? pb : pa, v2);\n        }\n    }\n    if (track) tdiag(step, 4);\n", 1),
     ("    const int P = a.B * a.C;\n    const int T = a.nbands", "    tdiag(step, 0);\n    const int P = a.B * a.C;\n    const int T = a.nbands", 1),
