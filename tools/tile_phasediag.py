@@ -87,3 +87,26 @@ print(f"tile B={B} {H}x{W}: {G} workgroups, {ms * 1e3:.1f} us per step (events, 
 for k in pb:
     print(f"  {k:>20s}: {pb[k]:7.2f} us   (previous launch {pa[k]:7.2f})")
 print(f"  {'gap to next launch':>20s}: {gap:7.2f} us")
+
+# Per-workgroup view of launch k (why the arrival spread): phase durations of the earliest and the latest arrivals,
+# the arrival spread per XCD (workgroups x and x + 8 share one) and the correlation of the arrival with each phase
+if os.environ.get("TDIAG_WG"):
+    L = Bq
+    t0 = L[:, 0].min()
+    work = np.where(L[:, 1] > 0)[0]
+    arr = us(L[work, 5] - t0)
+    cols = ["entry", "issue_noise", "loads", "iterations", "relerr_u2", "drain_arrive"]
+    ph = np.stack([us(L[work, 0] - t0)] + [us(L[work, i + 1] - L[work, i]) for i in range(5)], axis=1)
+    order = np.argsort(arr)
+    print("  per-workgroup phases (us): blockIdx | xcd | " + " | ".join(cols) + " | arrival")
+    for sel, name in ((order[:6], "earliest"), (order[-6:], "latest")):
+        print(f"  -- {name}")
+        for i in sel:
+            print("   %5d | %d | " % (work[i], work[i] & 7) + " | ".join(f"{v:6.2f}" for v in ph[i]) + f" | {arr[i]:6.2f}")
+    for x in range(8):
+        m = (work & 7) == x
+        if m.any():
+            print(f"  xcd {x}: {m.sum():3d} wgs, arrival {arr[m].min():6.2f} .. {arr[m].max():6.2f} us, mean {arr[m].mean():6.2f}")
+    for j, c in enumerate(cols):
+        if ph[:, j].std() > 0:
+            print(f"  corr(arrival, {c:>12s}) = {np.corrcoef(arr, ph[:, j])[0, 1]:+.2f}   std {ph[:, j].std():5.2f} us")
