@@ -11,6 +11,10 @@ One translation unit per kernel family (csrc/*.hip), compiled in parallel, then 
 kernels are bit-identical to the torch CPU checker); fmas are written explicitly
 where the fast kernels want them.
 
+tv_tile.hip adds -mllvm -amdgpu-sched-strategy=max-ilp (UNIT_FLAGS): the tile kernel is latency-bound at four
+waves per SIMD, and the ILP-first machine scheduler measured -1.7 % at 8 chains and -0.7 % for castle at batch 1
+(the row stream +0.3 %, so it keeps the default; profiles/r05s_sched_strategy_ab.txt).
+
 Diagnostic variants (tools/variant_build.py) rebuild only the units their patches touch.
 """
 from __future__ import annotations
@@ -32,6 +36,7 @@ OUT = os.path.join(PKG, "libpsgla_hip.so")
 OBJ = os.path.join(REPO, "build", "obj")
 ARCH = os.environ.get("PSGLA_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-Wno-inline-asm", "-fPIC"]
+UNIT_FLAGS = {"tv_tile": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
 
 
 def hipcc() -> str:
@@ -57,7 +62,8 @@ def compile_units(sources, objdir, extra=(), include=(), verbose=False):
 
     def one(src):
         obj = os.path.join(objdir, os.path.splitext(os.path.basename(src))[0] + ".o")
-        cmd = [hipcc(), f"--offload-arch={ARCH}"] + FLAGS + list(extra) + inc + ["-c", src, "-o", obj]
+        unit = os.path.splitext(os.path.basename(src))[0]
+        cmd = [hipcc(), f"--offload-arch={ARCH}"] + FLAGS + UNIT_FLAGS.get(unit, []) + list(extra) + inc + ["-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
