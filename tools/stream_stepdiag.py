@@ -47,5 +47,7 @@ per = lambda col: (d[:, col] / n).mean()  # noqa: E731
 print(f"stream B={B}: launch {ms*1e3:.1f} us (diag build); steps per workgroup {n.mean():.1f}")
 print(f"  per step (s_memtime ticks): length {per(1):.0f}")
 roles = ["front"] * 4 + [f"stage{k}" for k in range(1, 11)] + ["back"] * 2
+if os.environ.get("PSGLA_STREAM_LAYOUT") == "2":     # the merged layout of commit 8674423 (12 waves)
+    roles = ["front"] * 4 + ["st1+2", "st3+4", "st5+6", "st7+8", "stage9", "stage10"] + ["back"] * 2 + ["-"] * 4
 for w in range(16):
     print(f"  w{w:2d} {roles[w]:>7s}: work {per(4 + w):6.0f}   last to arrive in {100 * (d[:, 20 + w] / n).mean():5.1f} % of steps")
