@@ -233,7 +233,12 @@ static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
         int bh2 = 0, nb2 = 0, bh9 = 0, nb9 = 0;
         const int wg = tile_geometry(P, d->H, tile_segs, d->n_tv, 16, 3, &bh, &nb);
         const int wg2 = tile_geometry(P, d->H, tile_segs, d->n_tv, 16, 2, &bh2, &nb2);
-        const int wg9 = tile_geometry(P, d->H, tile_segs, d->n_tv, 8, 9, &bh9, &nb9);
+        // 72-row tiles (8 waves x 9 rows: 256 VGPRs at 2 waves per SIMD) only in fast mode at alpha = 1, the one
+        // instance that fits its registers (14-23 VGPRs spilled); exact mode and alpha != 1 spilled 50-422 VGPRs
+        // there, and the exact instance faulted / miscompared when its register allocation shifted:
+        // those cases take 48-row tiles in two rounds or the row stream instead (round 6)
+        const bool allow9 = !d->exact && d->x2[0] == nullptr;
+        const int wg9 = allow9 ? tile_geometry(P, d->H, tile_segs, d->n_tv, 8, 9, &bh9, &nb9) : 0;
         if (d->kernel_variant == 4 && wg == 0) { g_sel_err = "psgla_tv_step: shape not supported by the tile kernel"; return -1; }
         // auto: the tiles fit in one round on the CUs -- or in two when the rows need column segments (W > 256),
         // where the row stream's 256-column windows run a third of their lanes idle (measured: castle-size

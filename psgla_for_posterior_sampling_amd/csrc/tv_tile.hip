@@ -579,8 +579,11 @@ bool launch_tile(const TvArgs& s, dim3 grid, hipStream_t st, bool exact, bool al
         else hipLaunchKernelGGL((tv_tile_kernel<E, A, RV, true, NWV>), grid, dim3(NWV * WAVE), 0, st, s);      \
         return true; \
     }
-#define PSGLA_TILES(E, A) PSGLA_TILE(E, A, 16, 2) PSGLA_TILE(E, A, 16, 3) PSGLA_TILE(E, A, 8, 4) PSGLA_TILE(E, A, 8, 6) PSGLA_TILE(E, A, 8, 9)
+    // the instances select_step_kernel (api.hip) dispatches: 32- and 48-row tiles of 16 waves everywhere, 72-row
+    // tiles of 8 waves in fast mode at alpha = 1 only (the other 72-row instances spilled 50-422 VGPRs; round 6)
+#define PSGLA_TILES(E, A) PSGLA_TILE(E, A, 16, 2) PSGLA_TILE(E, A, 16, 3)
     PSGLA_TILES(true, true) PSGLA_TILES(true, false) PSGLA_TILES(false, true) PSGLA_TILES(false, false)
+    PSGLA_TILE(false, true, 8, 9)
 #undef PSGLA_TILES
 #undef PSGLA_TILE
     return false;

@@ -245,7 +245,9 @@ class FusedTvChains:
     def launch_main_only(self, n: int = 1):
         """Launch only the fused tile kernel n times for the CURRENT step (idempotent: it reads
         the step's inputs and rewrites the same outputs; the step counter does not move).
-        Used to time the dominant kernel alone."""
+        Used to time the dominant kernel alone.  A pending early-stop redo of the last step is settled first:
+        this launch rewrites the ping-pong buffer that redo reads its inputs from."""
+        self.settle()
         d = N.PsglaTvStep.from_buffer_copy(self.desc)
         d.launch_mask = 1
         for _ in range(n):
@@ -284,6 +286,8 @@ class FusedTvChains:
         """X_step, the input of step `step` -- intact in its ping-pong buffer until step + 1 has run."""
         if not (self.steps_done - 1 <= step <= self.steps_done):
             raise ValueError("only the last step's input is still held")
+        if step == self.steps_done:
+            self.settle()           # the last step's output: a pending early-stop redo rewrites it
         return self._view(self.x[step & 1])
 
     @property

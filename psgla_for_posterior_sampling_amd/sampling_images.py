@@ -140,6 +140,21 @@ def algorithm_parameters(pars, argv):
     return N, s, lambd, delta, n_inter, extras
 
 
+PLUMBING_RESIDUAL_SCALE = 1e-3
+
+
+@torch.no_grad()
+def plumbing_residual_scale_(conv: torch.nn.Conv2d, scale: float = PLUMBING_RESIDUAL_SCALE) -> None:
+    """A random-init DnCNN (no weights offline) stands in for the trained one in plumbing runs.  Raw, it is not a
+    denoiser: its default-init layers shrink the signal, so out_conv(h) + x is x plus out_conv's bias, about
+    ±0.04 per pixel and step, and the chain drifts without bound (PSNR_MMSE -21 dB after 1,000 steps).
+    Scaling the residual branch's output layer by 1e-3 keeps D = id + a small bounded residual, so the chain stays
+    on the observation's scale like a trained network's, and rounding differences between runs stay rounding."""
+    conv.weight.mul_(scale)
+    if conv.bias is not None:
+        conv.bias.mul_(scale)
+
+
 def make_denoiser(pars, device):
     if pars.den == "TV":
         return TVDenoiser(n_it_max=pars.den_TV_it)
@@ -150,7 +165,10 @@ def make_denoiser(pars, device):
         w = os.path.join(pars.weights_dir, "dncnn_sigma2_lipschitz_color.pth")
         if not os.path.exists(w) and not pars.allow_random_weights:
             raise FileNotFoundError(f"{w} not found (DnCNN weights; --allow_random_weights for plumbing runs)")
-        return DnCNN(in_channels=3, out_channels=3, pretrained=w if os.path.exists(w) else None, device=device)
+        net = DnCNN(in_channels=3, out_channels=3, pretrained=w if os.path.exists(w) else None, device=device)
+        if not os.path.exists(w):
+            plumbing_residual_scale_(net.out_conv)
+        return net
     if pars.den == "DRUNet":
         w = os.path.join(pars.weights_dir, "drunet_color.pth")
         if not os.path.exists(w) and not pars.allow_random_weights:

@@ -84,7 +84,7 @@ def test_bench_multirank_rehearsal():
     import subprocess
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    base = ["bench.py", "--steps", "20", "--warmup", "5", "--no-cpu", "--kernel-iters", "3", "--warmup-seconds", "0"]
+    base = ["bench.py", "--steps", "20", "--warmup", "5", "--no-cpu", "--warmup-seconds", "0"]
     env = dict(os.environ, PSGLA_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
     sock = socket.socket()
     sock.bind(("127.0.0.1", 0))
@@ -181,8 +181,18 @@ def test_cli_batched_and_sharded_equal_sequential(tmp_path, den):
     assert two.returncode == 0, two.stderr[-3000:]
     assert "Dataset (5 images): mean output PSNR" in two.stdout, two.stdout[-2000:]
     runs["ranks"] = _records(str(tmp_path / "ranks"), 5)
+    # the comparison is only meaningful on a bounded chain (a raw random DnCNN drifted to MMSE values of
+    # -23 .. 13 and amplified the conv rounding; the CLI's plumbing network is D = id + 1e-3 x residual)
+    for r in runs["seq"]:
+        assert np.abs(np.asarray(r["MMSE"])).max() < 2.0 and r["PSNR_MMSE"] > r["PSNR_y"] - 3.0, r["PSNR_MMSE"]
+    if den != "TV":
+        for tag in ("batch", "ranks"):
+            for k in ("MMSE", "std"):
+                d = max(float(np.max(np.abs(np.asarray(ra[k]) - np.asarray(rb[k])) / (np.abs(np.asarray(rb[k])) + 1e-5)))
+                        for ra, rb in zip(runs[tag], runs["seq"]))
+                print(f"DnCNN {tag} vs seq: max rel diff of {k} = {d:.3g}")
     # TV (the HIP step alone) is bit-identical; DnCNN's forward runs on MIOpen, whose convolution solver is
-    # chosen per batch size (B = 1, 2, 3 here), so its records agree to fp32 rounding (measured 6e-7 rel.)
+    # chosen per batch size (B = 1, 2, 3 here), so its records agree to fp32 rounding
     _same_records(runs["batch"], runs["seq"], exact=den == "TV")
     _same_records(runs["ranks"], runs["seq"], exact=den == "TV")
 

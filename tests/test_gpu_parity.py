@@ -812,7 +812,9 @@ def test_auto_dispatch_by_shape():
                                                   # enough tiles that 32-row tiles would need two rounds:
                                                   # 48-row tiles (3 rows per wave), plain and segmented
                                                   (12, 100, 64, 1.0, 1e-5, 10), (24, 40, 301, 1.0, 3e-2, 10),
-                                                  # and 48-row tiles too: 72-row tiles (8 waves x 9 rows)
+                                                  # more than one round of 48-row tiles: two rounds in exact
+                                                  # mode (72-row tiles are a fast-mode alpha = 1 instance only
+                                                  # since round 6; the fast one is pinned to the row stream below)
                                                   (24, 100, 64, 1.0, 1e-5, 10), (24, 130, 64, 1.0, 3e-2, 10),
                                                   # one- and two-row images, one inner iteration
                                                   (2, 1, 40, 1.0, 1e-5, 10), (1, 2, 321, 1.0, 1e-5, 10),
@@ -822,8 +824,8 @@ def test_tile_kernel_exact_vs_oracle(B, H, W, alpha, tol, n_tv):
     inline finalisation) in exact mode: samples, block means and TV state bit-identical to the CPU oracle
     for band cuts, narrow images (idle lanes), alpha != 1, deepinv's early stop and n_tv > 10; for rows
     padded to a pitch (W % 4 != 0) and column segments with n_tv halo columns (W > 256); 32-row tiles
-    where they fit on the CUs in one round, 48-row tiles for the larger batches, 72-row tiles of 8 waves
-    where 48-row ones would need a second round."""
+    where they fit on the CUs in one round, 48-row tiles for the larger batches, in two rounds where they
+    do not fit in one (the serial early-stop recompute)."""
     from psgla_for_posterior_sampling_amd.engine import FusedTvChains
     from psgla_for_posterior_sampling_amd import hip_ops as K
     g = torch.Generator().manual_seed(9)
@@ -991,3 +993,46 @@ def test_parallel_early_stop_redo_equals_serial(B, H, W, variant, stream_wgs):
             outs.append((eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone()))
         for a, b in zip(*outs):
             assert torch.equal(a, b), (tol, B, H, W, variant)
+
+
+@pytest.mark.parametrize("variant,B,H,W,stream_wgs", [("stream", 6, 40, 52, -1), ("tile", 2, 100, 64, 0),
+                                                      ("tile", 1, 61, 301, 0)])
+@pytest.mark.parametrize("exact,alpha,warm", [(True, 1.0, False), (False, 0.6, False), (True, 0.6, False),
+                                              (False, 1.0, True), (False, 0.6, True)])
+def test_parallel_early_stop_redo_modes(variant, B, H, W, stream_wgs, exact, alpha, warm):
+    """The parallel early-stop redo (ABI 11) on the paths the fast alpha = 1 cold-start cases above do not take
+    (ADVICE r5): exact arithmetic, the alpha != 1 TV primal ping-pong (x2) the redo must read from the stopped
+    step's parity, and a warm start from a previous run's (x2, u2), whose first step runs with its own descriptor
+    (step() settles it with that descriptor).  tol = 0.2: the stop fires on every chain in every step.
+    Parallel == serial recompute, bit for bit; input_state() of the last step is settled."""
+    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    g = torch.Generator(device=DEV).manual_seed(15)
+    xs = torch.rand((B, 3, H, W), generator=g, device=DEV)
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    mask2d = (torch.rand((H, W), generator=gen, device=DEV) > 0.5).to(torch.uint8)
+    y = mask2d.float() * xs
+    init = (mask2d.float() * y + (1 - mask2d.float()) * 0.5).contiguous()
+    tv_x2 = tv_u2 = None
+    if warm:
+        tv_x2 = (init + 0.01 * torch.rand(init.shape, generator=g, device=DEV)).contiguous()
+        tv_u2 = (0.02 * torch.rand(init.shape + (2,), generator=g, device=DEV) - 0.01).contiguous()
+    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
+    outs = []
+    for par in (True, False):
+        eng = FusedTvChains(init, y.contiguous(), mask2d, c1=c1, c2=c2, sigma2=float(np.float32((1 / 255.0) ** 2)),
+                            alpha=alpha, ths=float(np.float32(10 / 255.0)), tv=K.TvConstants(n_it_max=10, tol=0.2),
+                            seed=2, n_iter=16, n_inter=3, n_inter_mmse=4, kernel_variant=variant, exact=exact,
+                            stream_wgs=stream_wgs, parallel_redo=par, tv_x2=tv_x2, tv_u2=tv_u2)
+        assert eng.main_kernel == "tv_" + variant + "_kernel"
+        eng.run(4)
+        last_in = eng.input_state(eng.steps_done).clone()     # settles the pending redo of step 3
+        eng.run(12, graph_steps=4)
+        torch.cuda.synchronize()
+        eng.check_handoff()
+        assert int(eng.work.redo[0].item()) == 0 and int(eng.work.arrive[0].item()) == 0
+        bm, bm2 = eng.blocks()
+        outs.append((last_in, eng.samples().clone(), bm.clone(), bm2.clone(), eng.X.clone(), eng.u2_state.clone(),
+                     eng.x2_state.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b), (variant, exact, alpha, warm)

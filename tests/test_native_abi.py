@@ -73,9 +73,9 @@ def test_kernel_dispatch_rules_on_the_host():
     lib = N.lib()
     BAND, STREAM, TILE = 0, 1, 3
 
-    def kind(B, H, W, ldw=0, n_tv=10, variant=0, alpha1=True):
+    def kind(B, H, W, ldw=0, n_tv=10, variant=0, alpha1=True, exact=False):
         d = N.PsglaTvStep()
-        d.B, d.C, d.H, d.W, d.ldw, d.n_tv, d.kernel_variant = B, 3, H, W, ldw, n_tv, variant
+        d.B, d.C, d.H, d.W, d.ldw, d.n_tv, d.kernel_variant, d.exact = B, 3, H, W, ldw, n_tv, variant, int(exact)
         if not alpha1:
             d.x2[0], d.x2[1] = 16, 32          # non-null: alpha != 1 (the query never dereferences them)
         k = lib.psgla_tv_step_kernel(ctypes.byref(d))
@@ -86,6 +86,11 @@ def test_kernel_dispatch_rules_on_the_host():
     assert kind(12, 256, 256)[0] == TILE                         # 72-row tiles (8 waves x 9 rows): 180 tiles
     assert kind(16, 256, 256)[0] == TILE                         # 4-GPU strong split: 240 tiles of 72 rows
     assert kind(20, 256, 256)[0] == STREAM                       # 300 tiles of 72 rows: two rounds lose
+    # 72-row tiles only in fast mode at alpha = 1 (round 6: the other instances spilled)
+    assert kind(16, 256, 256, exact=True)[0] == STREAM
+    assert kind(16, 256, 256, alpha1=False)[0] == STREAM
+    assert kind(16, 256, 256, exact=True, variant=4)[0] == TILE  # forced: 48-row tiles in two rounds
+    assert kind(8, 256, 256, exact=True)[0] == TILE              # 48-row tiles in one round: every mode
     assert kind(64, 256, 256, alpha1=False)[0] == STREAM
     assert kind(1, 481, 321, ldw=324)[0] == TILE                 # castle at the CLI's batch 1
     assert kind(4, 481, 321, ldw=324)[0] == TILE                 # segmented rows: two rounds of tiles

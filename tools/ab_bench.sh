@@ -4,7 +4,7 @@
 # product library with that environment variable set (e.g. PSGLA_STREAM_LAYOUT=2); prodN@ARGS = the product library
 # with extra bench arguments ARGS (a leg named prodN).
 # stdout/stderr of every leg are kept (gpurun_out/ab_TAG/<lib>_<rep>.{json,err}); a failing leg ends the script
-# with its stderr printed.  One line per leg: tag | lib | rep | ms_per_step | kernel_ms | iso kernel_ms_isolated | kernel.
+# with its stderr printed.  One line per leg: tag | lib | rep | ms_per_step | kernel_ms | kernel.
 # Usage: tools/ab_bench.sh TAG REPS "BENCH ARGS" lib1 lib2 ...
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -25,7 +25,7 @@ for rep in $(seq 1 $REPS); do
 import json, sys
 t, v, rep, path = sys.argv[1:]
 d = json.loads(open(path).read().strip().splitlines()[-1])
-print(f"{t} | {v:>22s} | {rep} | {d['ms_per_step']:.5f} | {d['roofline']['kernel_ms']:.5f} | iso {d['roofline']['kernel_ms_isolated']:.5f} | {d['roofline']['kernel']}", flush=True)
+print(f"{t} | {v:>22s} | {rep} | {d['ms_per_step']:.5f} | {d['roofline']['kernel_ms']:.5f} | {d['roofline']['kernel']}", flush=True)
 PY
   done
 done

@@ -14,7 +14,7 @@ for v in "$@"; do
   for c in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE"; do
     i=$((i + 1))
     env $LIBENV timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $O/${v}_p$i -o p -- \
-      python3 bench.py --steps 40 --warmup 4 --warmup-seconds 0.3 --no-cpu --kernel-iters 5 $ARGS \
+      python3 bench.py --steps 40 --warmup 4 --warmup-seconds 0.3 --no-cpu $ARGS \
       > $O/${v}_p$i.json 2> $O/${v}_p$i.err || { echo "pmc $v $c failed"; tail -20 $O/${v}_p$i.err; exit 1; }
   done
   python3 tools/pmc_summary.py --round $T --kernel $K --out $O/${v}.json $O/${v}_p1 $O/${v}_p2 $O/${v}_p3 > /dev/null || exit 1

@@ -23,7 +23,7 @@ for c in "FETCH_SIZE" "WRITE_SIZE" \
          "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_DATA_FIFO_FULL SQ_INSTS_VALU_TRANS_F32"; do
   i=$((i + 1))
   timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $O/pmc$i -o p -- \
-    python3 bench.py --steps 40 --warmup 4 --warmup-seconds 0.3 --no-cpu --kernel-iters 5 $EXTRA > $O/bench_pmc$i.json
+    python3 bench.py --steps 40 --warmup 4 --warmup-seconds 0.3 --no-cpu $EXTRA > $O/bench_pmc$i.json
 done
 python3 tools/pmc_summary.py --round $R --kernel $KERNEL --chains $CHAINS --commit $COMMIT --command "python3 $CMD" \
   --out $O/pmc.json $O/pmc1 $O/pmc2 $O/pmc3 $O/pmc4
