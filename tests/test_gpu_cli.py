@@ -137,10 +137,12 @@ def _same_records(a, b, exact):
         for k in ("PSNR_sample", "PSNR_mmse", "SIM_sample", "MMSE", "std"):
             if exact:
                 np.testing.assert_array_equal(np.asarray(ra[k]), np.asarray(rb[k]), err_msg=k)
-            else:    # std = sqrt(E[X^2] - E[X]^2) amplifies the rounding by cancellation
-                tol = dict(rtol=1e-3, atol=1e-5) if k == "std" else dict(rtol=1e-5, atol=2e-6)
+            else:
+                # measured on the bounded plumbing chain (profiles/r06b_cli_dncnn.log): MMSE <= 1.4e-5 relative
+                # (1e-5 absolute floor in the denominator), std <= 5.5e-7; the bounds leave a 7x margin
+                tol = dict(rtol=1e-4, atol=1e-5)
                 np.testing.assert_allclose(np.asarray(ra[k]), np.asarray(rb[k]), err_msg=k, **tol)
-        assert (ra["PSNR_MMSE"] == rb["PSNR_MMSE"]) if exact else abs(ra["PSNR_MMSE"] - rb["PSNR_MMSE"]) < 1e-4
+        assert (ra["PSNR_MMSE"] == rb["PSNR_MMSE"]) if exact else abs(ra["PSNR_MMSE"] - rb["PSNR_MMSE"]) < 1e-3
 
 
 @pytest.mark.parametrize("den", ["DnCNN", "TV"])

@@ -7,7 +7,8 @@ Random-init networks (no weights offline), synthetic U[0,1) 3x256x256 images, th
 parameters (sampling_images.py:100-198): DnCNN s = 2/255, lambda = 5; PnP-ULA + DRUNet s1 = 5/255.
 Steps are hipGraph-replayed (engine.DenoiserChains / UlaChains).  Prints one JSON line: chain-steps/s,
 the denoiser's algorithmic TFLOP/s (layer-shape FLOPs, denoisers.py) against the fp32 peak, and the
-HIP epilogue kernel's share timed alone with HIP events."""
+denoiser forward timed alone with HIP events.  The HIP passes' own durations come from a rocprofv3 kernel trace
+of this command (tools/dnn_pass_roofline.py), not from a difference of wall times."""
 from __future__ import annotations
 
 import argparse
@@ -105,7 +106,7 @@ def main():
         "denoiser_ms": round(den_ms, 3), "denoiser_gflop_per_image": round(flops / 1e9, 2),
         "denoiser_tflops": round(tflops, 1), "fp32_peak_tflops": FP32_PEAK_TFLOPS,
         "denoiser_frac_of_peak": round(tflops / FP32_PEAK_TFLOPS, 3),
-        "hip_share_ms": round(ms - den_ms, 3), "miopen_find": a.find, "channels_last_flag": a.channels_last, "dtype": "f32", "weights": "random-init (none offline)",
+        "miopen_find": a.find, "channels_last_flag": a.channels_last, "dtype": "f32", "weights": "random-init (none offline)",
     }), flush=True)
 
 
