@@ -230,41 +230,37 @@ static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
         int bh = 0, nb = 0;
         // column segments as the stream kernel's (one when ldw == W <= 256)
         tile_segs = (a.ldw % 4 == 0 && d->n_tv >= 1) ? stream_segments(a.W, a.ldw, d->n_tv, &tile_sw) : 0;
-        int bh2 = 0, nb2 = 0, bh9 = 0, nb9 = 0;
-        const int wg = tile_geometry(P, d->H, tile_segs, d->n_tv, 16, 3, &bh, &nb);
+        // Shipped tile instances (round 6: none spills a VGPR -- a spill inside a divergent region loses the inactive
+        // lanes' values): 32-row tiles (16 waves x 2 rows) always, 48-row tiles (16 x 3) at alpha = 1
+        // only; the 72-row tiles (8 x 9) of rounds 4-5 are gone (12-16 chains take the row stream)
+        const bool alpha1 = d->x2[0] == nullptr;
+        int bh2 = 0, nb2 = 0;
+        const int wg3 = alpha1 ? tile_geometry(P, d->H, tile_segs, d->n_tv, 16, 3, &bh, &nb) : 0;
         const int wg2 = tile_geometry(P, d->H, tile_segs, d->n_tv, 16, 2, &bh2, &nb2);
-        // 72-row tiles (8 waves x 9 rows: 256 VGPRs at 2 waves per SIMD) only in fast mode at alpha = 1, the one
-        // instance that fits its registers (14-23 VGPRs spilled); exact mode and alpha != 1 spilled 50-422 VGPRs
-        // there, and the exact instance faulted / miscompared when its register allocation shifted:
-        // those cases take 48-row tiles in two rounds or the row stream instead (round 6)
-        const bool allow9 = !d->exact && d->x2[0] == nullptr;
-        const int wg9 = allow9 ? tile_geometry(P, d->H, tile_segs, d->n_tv, 8, 9, &bh9, &nb9) : 0;
-        if (d->kernel_variant == 4 && wg == 0) { g_sel_err = "psgla_tv_step: shape not supported by the tile kernel"; return -1; }
+        if (d->kernel_variant == 4 && wg3 == 0 && wg2 == 0) { g_sel_err = "psgla_tv_step: shape not supported by the tile kernel"; return -1; }
         // auto: the tiles fit in one round on the CUs -- or in two when the rows need column segments (W > 256),
         // where the row stream's 256-column windows run a third of their lanes idle (measured: castle-size
         // images at B = 3-4 and 321 x 481 at B = 4-6 run faster as two rounds of tiles; 256 x 256 does not,
         // profiles/r03l_tile_threshold.txt)
-        const long long ntiles = (long long)P * nb * tile_segs, cus = device_cus();
-        const long long ntiles9 = (long long)P * nb9 * tile_segs;
-        if (wg > 0 && (d->kernel_variant == 4 || ntiles <= cus || (wg9 > 0 && ntiles9 <= cus) ||
-                       (tile_segs > 1 && ntiles <= 2 * cus))) {
-            a.tile_r = 3;
-            a.tile_nw = 16;
-            a.band_h = bh;
-            a.nbands = nb;
-            // 72-row tiles (8 waves x 9 rows) when 48-row tiles would need a second round but these fit in one
-            if (ntiles > cus && wg9 > 0 && ntiles9 <= cus) {
-                a.tile_r = 9;
-                a.tile_nw = 8;
-                a.band_h = bh9;
-                a.nbands = nb9;
+        const long long cus = device_cus();
+        const long long ntiles = wg3 > 0 ? (long long)P * nb * tile_segs : (long long)P * nb2 * tile_segs;
+        const bool fits2 = wg2 > 0 && (long long)P * nb2 * tile_segs <= cus;
+        if ((wg3 > 0 || wg2 > 0) && (d->kernel_variant == 4 || ntiles <= cus || fits2 || (tile_segs > 1 && ntiles <= 2 * cus))) {
+            if (wg3 > 0) {
+                a.tile_r = 3;
+                a.band_h = bh;
+                a.nbands = nb;
+            } else {
+                a.tile_r = 2;
+                a.band_h = bh2;
+                a.nbands = nb2;
             }
+            a.tile_nw = 16;
             // 32-row tiles (2 rows per wave) when they still fit in one round: one or a few images leave most
             // CUs idle at 48 rows (castle B = 1: 114 tiles of 48 rows vs 246 of 32 rows, 41.1 -> 35.0 us,
             // profiles/r03q_tile_r2_ab.txt); more tiles but shorter waves
-            if (wg2 > 0 && (long long)P * nb2 * tile_segs <= cus) {
+            if (fits2) {
                 a.tile_r = 2;
-                a.tile_nw = 16;
                 a.band_h = bh2;
                 a.nbands = nb2;
             }
@@ -334,6 +330,7 @@ int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream) {
     a.yobs = d->y; a.y_cs = d->y_chain_stride; a.mask = d->mask; a.m_cs = d->mask_chain_stride;
     a.c1 = d->c1; a.c2 = d->c2; a.sigma2 = d->sigma2; a.alpha = d->alpha;
     a.tau = d->tau; a.opt = d->one_plus_tau; a.inv_opt = (float)(1.0 / (double)d->one_plus_tau);
+    a.tau_opt = (float)((double)d->tau / (double)d->one_plus_tau);
     a.sig_tv = d->sigma_tv; a.rho = d->rho; a.ths = d->ths; a.tol = d->tol;
     a.inv_sigma2 = (float)(1.0 / (double)a.sigma2);
     a.n_tv = d->n_tv; a.seed = d->seed; a.chain0 = d->chain0; a.pingpong = 1;
@@ -381,6 +378,7 @@ int psgla_tv_prox(const PsglaTvProx* d, void* stream) {
     a.x2[0] = const_cast<float*>(d->x2_in); a.x2[1] = d->x2_out;
     a.u2[0] = const_cast<float*>(d->u2_in); a.u2[1] = d->u2_out;
     a.tau = d->tau; a.opt = d->one_plus_tau; a.inv_opt = (float)(1.0 / (double)d->one_plus_tau);
+    a.tau_opt = (float)((double)d->tau / (double)d->one_plus_tau);
     a.sig_tv = d->sigma_tv; a.rho = d->rho; a.ths = d->ths; a.tol = d->tol;
     a.n_tv = d->n_tv; a.pingpong = 0;
     a.fresh_host = d->fresh; a.per_chain_norm = d->per_chain ? 1 : 0; a.norms = d->norms; a.arrive = d->arrive;

@@ -78,11 +78,13 @@ __device__ __forceinline__ void bl_load_row(const float* p, float (&row)[SEG * 4
     }
 }
 
-// One workgroup per (plane, tile), 1-D grid; three resident per CU for l <= 4 (168 VGPRs, 47 KB of LDS).
+// One workgroup per (plane, tile), 1-D grid; two resident per CU for l <= 4 (<= 256 VGPRs, 47 KB of LDS).
+// Round 6: three per CU (168 VGPRs) spilled 9 VGPRs to scratch, and a VGPR spill inside a divergent (exec-masked)
+// region loses the inactive lanes' values -- no shipped kernel spills (tests/test_native_abi.py).
 // (A persistent variant that DMA'd the next tile into a second buffer during the passes measured slower:
 // two workgroups per CU hide less than three)
 #ifndef PSGLA_BLUR_WPE
-#define PSGLA_BLUR_WPE 3
+#define PSGLA_BLUR_WPE 2
 #endif
 template <bool EXACT, int L>
 __global__ void __launch_bounds__(BL_THREADS, (L <= 4 ? PSGLA_BLUR_WPE : 1)) blur_grad_kernel(const BlurArgs a) {
@@ -509,12 +511,16 @@ static bool blur_rank1(const float* h, int K, float* r, float* c) {
     return true;
 }
 
+// Fast mode with l >= 7 (15 x 15 and 17 x 17 stencils that are not rank-1: never the reference's kernels, which are)
+// takes the exact-order kernel: the fast 2-D instances of those sizes spilled VGPRs to scratch (round 6)
 template <bool EXACT>
 static void launch_blur(const BlurArgs& a, int l, dim3 grid, hipStream_t st) {
     switch (l) {
 #define PSGLA_BLUR_CASE(LL) case LL: hipLaunchKernelGGL((blur_grad_kernel<EXACT, LL>), grid, dim3(BL_THREADS), 0, st, a); break;
+#define PSGLA_BLUR_CASE_X(LL) case LL: hipLaunchKernelGGL((blur_grad_kernel<true, LL>), grid, dim3(BL_THREADS), 0, st, a); break;
         PSGLA_BLUR_CASE(0) PSGLA_BLUR_CASE(1) PSGLA_BLUR_CASE(2) PSGLA_BLUR_CASE(3) PSGLA_BLUR_CASE(4)
-        PSGLA_BLUR_CASE(5) PSGLA_BLUR_CASE(6) PSGLA_BLUR_CASE(7) PSGLA_BLUR_CASE(8)
+        PSGLA_BLUR_CASE(5) PSGLA_BLUR_CASE(6) PSGLA_BLUR_CASE_X(7) PSGLA_BLUR_CASE_X(8)
+#undef PSGLA_BLUR_CASE_X
 #undef PSGLA_BLUR_CASE
         default: break;
     }

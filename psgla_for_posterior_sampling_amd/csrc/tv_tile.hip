@@ -121,7 +121,8 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
                 const float g = (mk[k] * (yo[k] - X[k])) * a.inv_sigma2;
                 Y = __builtin_fmaf(a.c2, Zn[r][k], __builtin_fmaf(a.c1, g, X[k]));
             }
-            yv[r][k] = ok ? Y : 0.f;
+            // fast mode at alpha = 1: the TV anchor held as tau_opt Y (the stream kernel's; round 6)
+            yv[r][k] = ok ? ((ALPHA1 && !EXACT) ? a.tau_opt * Y : Y) : 0.f;
             x2[r][k] = ok ? (fresh ? Y : (ALPHA1 ? X[k] : xs[k])) : 0.f;
             u0[r][k] = (ok && !fresh) ? us0[k] : 0.f;
             u1[r][k] = (ok && !fresh) ? us1[k] : 0.f;
@@ -242,6 +243,10 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
                     xv = ((xo - a.tau * tt) + a.tau * yv[r][k]) / a.opt;
                     zv = 2.0f * xv - xo;
                     xn = xo + a.rho * (xv - xo);
+                } else if (ALPHA1) {
+                    xv = __builtin_fmaf(a.inv_opt, xo, __builtin_fmaf(-a.tau_opt, tt, yv[r][k]));
+                    zv = __builtin_fmaf(2.0f, xv, -xo);
+                    xn = __builtin_fmaf(a.rho, xv - xo, xo);
                 } else {
                     xv = __builtin_fmaf(a.tau, yv[r][k] - tt, xo) * a.inv_opt;
                     zv = __builtin_fmaf(2.0f, xv, -xo);
@@ -579,11 +584,12 @@ bool launch_tile(const TvArgs& s, dim3 grid, hipStream_t st, bool exact, bool al
         else hipLaunchKernelGGL((tv_tile_kernel<E, A, RV, true, NWV>), grid, dim3(NWV * WAVE), 0, st, s);      \
         return true; \
     }
-    // the instances select_step_kernel (api.hip) dispatches: 32- and 48-row tiles of 16 waves everywhere, 72-row
-    // tiles of 8 waves in fast mode at alpha = 1 only (the other 72-row instances spilled 50-422 VGPRs; round 6)
-#define PSGLA_TILES(E, A) PSGLA_TILE(E, A, 16, 2) PSGLA_TILE(E, A, 16, 3)
+    // the instances select_step_kernel (api.hip) dispatches -- none spills a VGPR (round 6; checked by
+    // tests/test_native_abi.py): 32-row tiles everywhere, 48-row tiles at alpha = 1 (alpha != 1 spilled 1-12 VGPRs);
+    // no 72-row tiles (8 waves x 9 rows spilled 11-68 VGPRs at 256)
+#define PSGLA_TILES(E, A) PSGLA_TILE(E, A, 16, 2)
     PSGLA_TILES(true, true) PSGLA_TILES(true, false) PSGLA_TILES(false, true) PSGLA_TILES(false, false)
-    PSGLA_TILE(false, true, 8, 9)
+    PSGLA_TILE(true, true, 16, 3) PSGLA_TILE(false, true, 16, 3)
 #undef PSGLA_TILES
 #undef PSGLA_TILE
     return false;

@@ -777,7 +777,7 @@ def test_fused_single_channel_exact_vs_oracle(variant):
 
 def test_auto_dispatch_by_shape():
     """64 chains x 3 x 256 x 256 (BASELINE configs[1], one GPU): auto dispatch picks the row stream; 8 chains
-    (the 8-GPU strong split) and 16 (the 4-GPU split) the tile kernel; alpha != 1 and many chains of a real shape the row stream; one
+    (the 8-GPU strong split) the tile kernel; alpha != 1 and many chains of a real shape the row stream; one
     or two chains of a real shape (padded rows, column segments) the tile kernel."""
     from psgla_for_posterior_sampling_amd.engine import FusedTvChains
     from psgla_for_posterior_sampling_amd import hip_ops as K
@@ -795,10 +795,11 @@ def test_auto_dispatch_by_shape():
     assert kern(2, 321, 481) == "tv_tile_kernel"
     assert kern(4, 481, 321) == "tv_tile_kernel"        # two rounds of tiles beat segmented row streams
     assert kern(8, 481, 321) == "tv_stream_kernel"
-    # unsegmented rows: one round of tiles at most -- 72-row tiles (8 waves x 9 rows) where 48-row ones need two
-    assert kern(12, 256, 256) == "tv_tile_kernel"       # 36 planes x 5 bands
-    assert kern(16, 256, 256) == "tv_tile_kernel"       # the 4-GPU strong split: 48 planes x 5 bands
-    assert kern(20, 256, 256) == "tv_stream_kernel"     # 300 tiles of 72 rows: more than the CUs
+    # unsegmented rows: one round of tiles at most; since round 6 no 72-row tiles (they spilled VGPRs),
+    # so 12-16 chains (48-row tiles in two rounds) take the row stream
+    assert kern(12, 256, 256) == "tv_stream_kernel"
+    assert kern(16, 256, 256) == "tv_stream_kernel"     # the 4-GPU strong split
+    assert kern(8, 256, 256, alpha=0.6) == "tv_stream_kernel"   # 48-row tiles only at alpha = 1
 
 
 # ------------------------------------------------------------------------------ small-batch tile kernel
@@ -812,9 +813,8 @@ def test_auto_dispatch_by_shape():
                                                   # enough tiles that 32-row tiles would need two rounds:
                                                   # 48-row tiles (3 rows per wave), plain and segmented
                                                   (12, 100, 64, 1.0, 1e-5, 10), (24, 40, 301, 1.0, 3e-2, 10),
-                                                  # more than one round of 48-row tiles: two rounds in exact
-                                                  # mode (72-row tiles are a fast-mode alpha = 1 instance only
-                                                  # since round 6; the fast one is pinned to the row stream below)
+                                                  # more than one round of 48-row tiles: two rounds (the
+                                                  # serial early-stop recompute; no 72-row tiles since round 6)
                                                   (24, 100, 64, 1.0, 1e-5, 10), (24, 130, 64, 1.0, 3e-2, 10),
                                                   # one- and two-row images, one inner iteration
                                                   (2, 1, 40, 1.0, 1e-5, 10), (1, 2, 321, 1.0, 1e-5, 10),
@@ -919,7 +919,7 @@ def test_tile_kernel_equals_stream_kernel_real_shapes(B, H, W):
 def test_tile_kernel_early_stop_handoff_full_size(B, H, W, tol):
     """The tile kernel's fence-free step hand-off (sc1 stores, rel-err sums as agent atomics read back by
     the last workgroup's agent atomics) under a tolerance at which deepinv's early stop fires: 40 steps of
-    8 chains (48-row tiles) or 16 chains (72-row tiles) at 3 x 256 x 256, the reference's real shapes at
+    8 chains (48-row tiles) or 16 chains (48-row tiles in two rounds: the serial recompute) at 3 x 256 x 256, the reference's real shapes at
     the CLI's batch sizes (castle 481 x 321 at B = 1, 321 x 481 at B = 2) and 256 x 256 at B = 1, 2 (32-row
     tiles): >= 64 tiles per chain, so the rel-err sums are spread over the workspace's 8 norm copies (ABI 8;
     read back to back and reset by exchange since round 4), bit-identical to the row-streaming
@@ -965,8 +965,8 @@ def test_parallel_early_stop_redo_equals_serial(B, H, W, variant, stream_wgs):
     tol = 0.2 makes the stop fire on every
     chain in every step (after 3 inner iterations), tol = 2e-3 on some steps only; fast kernels, hipGraph replay,
     the bench shape (64 chains: row split, 256 workgroups), the castle shape at 64 chains (half-wave windows,
-    segments), per-plane streams, the 8-chain tile kernel, castle at batch 1 and 72-row tiles of 8 waves (two-phase
-    arrival): bit-identical."""
+    segments), per-plane streams, the 8-chain tile kernel, castle at batch 1 and 48-row tiles in two rounds (the
+    serial recompute in both legs): bit-identical."""
     from psgla_for_posterior_sampling_amd.engine import FusedTvChains
     from psgla_for_posterior_sampling_amd import hip_ops as K
     g = torch.Generator(device=DEV).manual_seed(5)

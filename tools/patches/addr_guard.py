@@ -15,7 +15,6 @@ __device__ __forceinline__ bool guard_bad(const void* p, int prim) {
 }
 '''
 PATCHES = [
-    ("typedef __attribute__((address_space(1))) const void* gptr_t;", GUARD + "typedef __attribute__((address_space(1))) const void* gptr_t;", 1),
     ("""__device__ __forceinline__ void glds16(const void* src, void* dst) {
     const unsigned off""", """__device__ __forceinline__ void glds16(const void* src, void* dst) {
     if (guard_bad(src, 0)) return;
@@ -39,6 +38,16 @@ PATCHES = [
     ("void launch_stream(const TvArgs& s, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen, bool half) {",
      """extern "C" int psgla_guard_set(void* p) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_guard_buf), &p, sizeof(p)); }
 void launch_stream(const TvArgs& s, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen, bool half) {""", 1),
+    ("__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }",
+     GUARD + """__device__ __forceinline__ float4 ld4(const float* p) {
+    if (guard_bad(p, 5)) return make_float4(0.f, 0.f, 0.f, 0.f);
+    return *reinterpret_cast<const float4*>(p);
+}""", 1),
+    ("            fM[r] = *reinterpret_cast<const uint32_t*>(a.mask + (size_t)b * a.m_cs + (size_t)gi[r] * L + gj0);",
+     "            fM[r] = guard_bad(a.mask + (size_t)b * a.m_cs + (size_t)gi[r] * L + gj0, 6) ? 0u : *reinterpret_cast<const uint32_t*>(a.mask + (size_t)b * a.m_cs + (size_t)gi[r] * L + gj0);", 1),
+    ("bool launch_tile(const TvArgs& s, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen) {",
+     """extern "C" int psgla_guard_set_tile(void* p) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_guard_buf), &p, sizeof(p)); }
+bool launch_tile(const TvArgs& s, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen) {""", 1),
     ("""    const long long step = launch_step(a);
     const bool fresh = launch_fresh(a);
     // the previous step's pending early-stop redo (rare): all workgroups in parallel, then one grid barrier;""",
