@@ -330,7 +330,6 @@ int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream) {
     a.yobs = d->y; a.y_cs = d->y_chain_stride; a.mask = d->mask; a.m_cs = d->mask_chain_stride;
     a.c1 = d->c1; a.c2 = d->c2; a.sigma2 = d->sigma2; a.alpha = d->alpha;
     a.tau = d->tau; a.opt = d->one_plus_tau; a.inv_opt = (float)(1.0 / (double)d->one_plus_tau);
-    a.tau_opt = (float)((double)d->tau / (double)d->one_plus_tau);
     a.sig_tv = d->sigma_tv; a.rho = d->rho; a.ths = d->ths; a.tol = d->tol;
     a.inv_sigma2 = (float)(1.0 / (double)a.sigma2);
     a.n_tv = d->n_tv; a.seed = d->seed; a.chain0 = d->chain0; a.pingpong = 1;
@@ -378,7 +377,6 @@ int psgla_tv_prox(const PsglaTvProx* d, void* stream) {
     a.x2[0] = const_cast<float*>(d->x2_in); a.x2[1] = d->x2_out;
     a.u2[0] = const_cast<float*>(d->u2_in); a.u2[1] = d->u2_out;
     a.tau = d->tau; a.opt = d->one_plus_tau; a.inv_opt = (float)(1.0 / (double)d->one_plus_tau);
-    a.tau_opt = (float)((double)d->tau / (double)d->one_plus_tau);
     a.sig_tv = d->sigma_tv; a.rho = d->rho; a.ths = d->ths; a.tol = d->tol;
     a.n_tv = d->n_tv; a.pingpong = 0;
     a.fresh_host = d->fresh; a.per_chain_norm = d->per_chain ? 1 : 0; a.norms = d->norms; a.arrive = d->arrive;

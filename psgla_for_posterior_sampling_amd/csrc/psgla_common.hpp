@@ -95,7 +95,6 @@ struct TvArgs {
     float c1, c2, sigma2, alpha;
     float inv_sigma2;               // fast kernels: 1/sigma2 (the data term multiplies)
     float tau, opt, inv_opt, sig_tv, rho, ths, tol;
-    float tau_opt;                  // fast kernels at alpha = 1: tau / (1 + tau); the TV anchor is held as tau_opt * Y
     int n_tv;
     unsigned long long seed;
     int chain0;

@@ -154,8 +154,6 @@ __device__ __forceinline__ void tv_tile(const TvArgs& a, int plane, int tile, in
             }
             yst = make_float4(colok[0] ? Yv[0] : 0.f, colok[1] ? Yv[1] : 0.f, colok[2] ? Yv[2] : 0.f,
                               colok[3] ? Yv[3] : 0.f);
-            if (ALPHA1 && !EXACT)   // fast mode at alpha = 1: the TV anchor held as tau_opt Y (the stream kernel's)
-                yst = make_float4(a.tau_opt * yst.x, a.tau_opt * yst.y, a.tau_opt * yst.z, a.tau_opt * yst.w);
         }
         *reinterpret_cast<float4*>(&sh.ylds[w * R + r][CPL * lane]) = yst;
     }
@@ -188,10 +186,6 @@ __device__ __forceinline__ void tv_tile(const TvArgs& a, int plane, int tile, in
                     xv = ((xo - a.tau * t) + a.tau * f4get(yrow, k)) / a.opt;
                     zv = 2.0f * xv - xo;
                     xn = xo + a.rho * (xv - xo);
-                } else if (ALPHA1) {
-                    xv = __builtin_fmaf(a.inv_opt, xo, __builtin_fmaf(-a.tau_opt, t, f4get(yrow, k)));
-                    zv = __builtin_fmaf(2.0f, xv, -xo);
-                    xn = __builtin_fmaf(a.rho, xv - xo, xo);
                 } else {
                     xv = __builtin_fmaf(a.tau, f4get(yrow, k) - t, xo) * a.inv_opt;
                     zv = __builtin_fmaf(2.0f, xv, -xo);

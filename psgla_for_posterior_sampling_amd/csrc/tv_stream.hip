@@ -245,7 +245,7 @@ struct StageRow {
     int lk;                   // GEN: the row's lastk (its column segment's), set by the primal
 };
 
-template <bool EXACT, bool TRK, bool GEN = false, bool HALF = false, bool A1 = false>
+template <bool EXACT, bool TRK, bool GEN = false, bool HALF = false>
 __device__ __forceinline__ void stage_phase_a(const TvArgs& a, const float4& X2, const float4& U0,
                                               const float4& U1, const float4& YY, const float (&pu0)[CPL],
                                               StageRow& o, float& sd, float& sn, int nreal = CPL) {
@@ -270,11 +270,6 @@ __device__ __forceinline__ void stage_phase_a(const TvArgs& a, const float4& X2,
             xv = ((xo - a.tau * tt) + a.tau * yy[kk]) / a.opt;
             zv = 2.0f * xv - xo;
             xn = xo + a.rho * (xv - xo);
-        } else if (A1) {
-            // (x2 - tau tt + tau Y) / (1 + tau) with the anchor held as tau_opt Y (round 6: one VALU fewer)
-            xv = __builtin_fmaf(a.inv_opt, xo, __builtin_fmaf(-a.tau_opt, tt, yy[kk]));
-            zv = __builtin_fmaf(2.0f, xv, -xo);
-            xn = __builtin_fmaf(a.rho, xv - xo, xo);
         } else {
             xv = __builtin_fmaf(a.tau, yy[kk] - tt, xo) * a.inv_opt;
             zv = __builtin_fmaf(2.0f, xv, -xo);
@@ -401,7 +396,7 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamSharedT<A1>& s
     auto primal = [&](int j, const float4& X2, const float4& U0, const float4& U1, const float4& YY,
                       const float (&pu0)[CPL], StageRow& cur) {
         float rd = 0.f, rn = 0.f;
-        stage_phase_a<EXACT, TRK, GEN, HALF, A1>(a, X2, U0, U1, YY, pu0, cur, rd, rn, nreal);
+        stage_phase_a<EXACT, TRK, GEN, HALF>(a, X2, U0, U1, YY, pu0, cur, rd, rn, nreal);
         if (GEN) cur.lk = lastk;
         if (TRK && j >= qc0 && j < qc1) { lsd += rd; lsn += rn; }
     };
@@ -412,11 +407,15 @@ __device__ __forceinline__ void stage_loop(const TvArgs& a, StreamSharedT<A1>& s
         float4 A, B;
         YY = sh.y[j & (SP_YRING - 1)][lane];
         if (FIRST) {
-            // the front's staging of row j (x2 = X, u2); on a TV restart (fresh) the front has overwritten it with
-            // x2 = Y, u2 = 0 (round 6: no selects here; lanes beyond the image never feed an image column)
-            X2 = sh.stX(j & 3, j)[lane];
-            A = sh.stUa(j & 3, j)[lane];
-            B = sh.stUb(j & 3, j)[lane];
+            // the front's staging of row j (x2 = X, u2); a TV restart (fresh): x2 = Y, u2 = 0 (selects, no branch
+            // around the LDS reads; lanes beyond the image read DMA'd values: they never feed an image column)
+            const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 sX = sh.stX(j & 3, j)[lane];
+            const float4 sA = sh.stUa(j & 3, j)[lane];
+            const float4 sB = sh.stUb(j & 3, j)[lane];
+            X2 = sel4(fresh, YY, sX);
+            A = sel4(fresh, zero4, sA);
+            B = sel4(fresh, zero4, sB);
         } else {
             const int sl = j & 1;
             X2 = sh.x2[rin][sl][lane];
@@ -646,19 +645,7 @@ __device__ __forceinline__ void stream_pass(const TvArgs& a, StreamSharedT<ALPHA
                     sh.ua[0][s0][lane] = sel4(fresh, zero4, sA);
                     sh.ub[0][s0][lane] = sel4(fresh, zero4, sB);
                 }
-                if (ALPHA1) {
-                    // stage 1 reads its TV input from this row's staging: a TV restart (fresh) puts x2 = Y, u2 = 0 there
-                    if (fresh) {
-                        sh.stX(fw, q)[lane] = Y4;
-                        sh.stUa(fw, q)[lane] = zero4;
-                        sh.stUb(fw, q)[lane] = zero4;
-                    }
-                    // the fast primal's anchor: tau_opt Y
-                    sh.y[q & (SP_YRING - 1)][lane] = EXACT ? Y4 : make_float4(a.tau_opt * Y4.x, a.tau_opt * Y4.y,
-                                                                              a.tau_opt * Y4.z, a.tau_opt * Y4.w);
-                } else {
-                    sh.y[q & (SP_YRING - 1)][lane] = Y4;
-                }
+                sh.y[q & (SP_YRING - 1)][lane] = Y4;
                 // the wave's next rows: noise row q + 4, DMA of row q + 8... issued as q + 4
                 front_issue(3, q + 4, rc_dma);
                 cursor_advance<GEN, HALF>(a, rm, rc_cur, 4);

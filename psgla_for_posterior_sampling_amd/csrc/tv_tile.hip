@@ -121,8 +121,7 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
                 const float g = (mk[k] * (yo[k] - X[k])) * a.inv_sigma2;
                 Y = __builtin_fmaf(a.c2, Zn[r][k], __builtin_fmaf(a.c1, g, X[k]));
             }
-            // fast mode at alpha = 1: the TV anchor held as tau_opt Y (the stream kernel's; round 6)
-            yv[r][k] = ok ? ((ALPHA1 && !EXACT) ? a.tau_opt * Y : Y) : 0.f;
+            yv[r][k] = ok ? Y : 0.f;
             x2[r][k] = ok ? (fresh ? Y : (ALPHA1 ? X[k] : xs[k])) : 0.f;
             u0[r][k] = (ok && !fresh) ? us0[k] : 0.f;
             u1[r][k] = (ok && !fresh) ? us1[k] : 0.f;
@@ -243,10 +242,6 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
                     xv = ((xo - a.tau * tt) + a.tau * yv[r][k]) / a.opt;
                     zv = 2.0f * xv - xo;
                     xn = xo + a.rho * (xv - xo);
-                } else if (ALPHA1) {
-                    xv = __builtin_fmaf(a.inv_opt, xo, __builtin_fmaf(-a.tau_opt, tt, yv[r][k]));
-                    zv = __builtin_fmaf(2.0f, xv, -xo);
-                    xn = __builtin_fmaf(a.rho, xv - xo, xo);
                 } else {
                     xv = __builtin_fmaf(a.tau, yv[r][k] - tt, xo) * a.inv_opt;
                     zv = __builtin_fmaf(2.0f, xv, -xo);
