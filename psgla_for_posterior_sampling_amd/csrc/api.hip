@@ -238,14 +238,13 @@ static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
         const int wg3 = alpha1 ? tile_geometry(P, d->H, tile_segs, d->n_tv, 16, 3, &bh, &nb) : 0;
         const int wg2 = tile_geometry(P, d->H, tile_segs, d->n_tv, 16, 2, &bh2, &nb2);
         if (d->kernel_variant == 4 && wg3 == 0 && wg2 == 0) { g_sel_err = "psgla_tv_step: shape not supported by the tile kernel"; return -1; }
-        // auto: the tiles fit in one round on the CUs -- or in two when the rows need column segments (W > 256),
-        // where the row stream's 256-column windows run a third of their lanes idle (measured: castle-size
-        // images at B = 3-4 and 321 x 481 at B = 4-6 run faster as two rounds of tiles; 256 x 256 does not,
-        // profiles/r03l_tile_threshold.txt)
+        // auto: the tiles fit in one or two rounds on the CUs (measured: castle-size images at B = 3-4 and 321 x 481 at
+        // B = 4-6 run faster as two rounds of tiles, profiles/r03l_tile_threshold.txt; since round 6, without the
+        // 72-row tiles, 16 chains at 256 x 256 too: 0.0644 vs 0.0680 ms, 12 chains even, profiles/r06m_tile_rounds_ab.txt)
         const long long cus = device_cus();
         const long long ntiles = wg3 > 0 ? (long long)P * nb * tile_segs : (long long)P * nb2 * tile_segs;
         const bool fits2 = wg2 > 0 && (long long)P * nb2 * tile_segs <= cus;
-        if ((wg3 > 0 || wg2 > 0) && (d->kernel_variant == 4 || ntiles <= cus || fits2 || (tile_segs > 1 && ntiles <= 2 * cus))) {
+        if ((wg3 > 0 || wg2 > 0) && (d->kernel_variant == 4 || ntiles <= 2 * cus || fits2)) {
             if (wg3 > 0) {
                 a.tile_r = 3;
                 a.band_h = bh;

@@ -777,7 +777,7 @@ def test_fused_single_channel_exact_vs_oracle(variant):
 
 def test_auto_dispatch_by_shape():
     """64 chains x 3 x 256 x 256 (BASELINE configs[1], one GPU): auto dispatch picks the row stream; 8 chains
-    (the 8-GPU strong split) the tile kernel; alpha != 1 and many chains of a real shape the row stream; one
+    (the 8-GPU strong split) and 16 (the 4-GPU split) the tile kernel; alpha != 1 and many chains of a real shape the row stream; one
     or two chains of a real shape (padded rows, column segments) the tile kernel."""
     from psgla_for_posterior_sampling_amd.engine import FusedTvChains
     from psgla_for_posterior_sampling_amd import hip_ops as K
@@ -795,10 +795,10 @@ def test_auto_dispatch_by_shape():
     assert kern(2, 321, 481) == "tv_tile_kernel"
     assert kern(4, 481, 321) == "tv_tile_kernel"        # two rounds of tiles beat segmented row streams
     assert kern(8, 481, 321) == "tv_stream_kernel"
-    # unsegmented rows: one round of tiles at most; since round 6 no 72-row tiles (they spilled VGPRs),
-    # so 12-16 chains (48-row tiles in two rounds) take the row stream
-    assert kern(12, 256, 256) == "tv_stream_kernel"
-    assert kern(16, 256, 256) == "tv_stream_kernel"     # the 4-GPU strong split
+    # since round 6 no 72-row tiles (they spilled VGPRs): 12-16 chains run 48-row tiles in two rounds
+    assert kern(12, 256, 256) == "tv_tile_kernel"
+    assert kern(16, 256, 256) == "tv_tile_kernel"       # the 4-GPU strong split: 480 tiles
+    assert kern(20, 256, 256) == "tv_stream_kernel"     # 600 tiles: three rounds
     assert kern(8, 256, 256, alpha=0.6) == "tv_stream_kernel"   # 48-row tiles only at alpha = 1
 
 

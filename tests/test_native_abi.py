@@ -84,8 +84,9 @@ def test_kernel_dispatch_rules_on_the_host():
     assert kind(64, 256, 256)[0] == STREAM                       # BASELINE configs[1], one GPU
     assert kind(8, 256, 256)[0] == TILE                          # 8-GPU strong split: 240 tiles
     # round 6: no 72-row tiles, 48-row tiles at alpha = 1 only (the other instances spilled VGPRs)
-    assert kind(12, 256, 256)[0] == STREAM
-    assert kind(16, 256, 256)[0] == STREAM                       # 4-GPU strong split
+    assert kind(12, 256, 256)[0] == TILE                         # 48-row tiles in two rounds
+    assert kind(16, 256, 256)[0] == TILE                         # 4-GPU strong split: 480 tiles
+    assert kind(20, 256, 256)[0] == STREAM                       # 600 tiles: three rounds
     assert kind(16, 256, 256, exact=True, variant=4)[0] == TILE  # forced: 48-row tiles in two rounds
     assert kind(8, 256, 256, exact=True)[0] == TILE              # 48-row tiles in one round: both modes
     assert kind(8, 256, 256, alpha1=False)[0] == STREAM          # alpha != 1: 32-row tiles would need 528
