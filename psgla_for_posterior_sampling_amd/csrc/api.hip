@@ -50,6 +50,16 @@ static int device_cus() {
     return cus;
 }
 
+// The parallel early-stop redo meets at a grid barrier (grid_sync), so every workgroup of the grid must be resident at
+// once: a grid within the CUs and within the instance's occupancy x the CUs.  Otherwise the finalising
+// workgroup recomputes stopped chains serially.  (The barrier's spin is bounded: an expired guard sets arrive[3],
+// which FusedTvChains.check_handoff raises on -- another process's kernels holding CUs for the whole guard is the
+// case the occupancy query cannot see.)
+static bool grid_resident(long long grid, int per_cu) {
+    const long long cus = device_cus();
+    return per_cu > 0 && grid <= cus && grid <= (long long)per_cu * cus;
+}
+
 // Row-split workgroup count for the streaming kernel (0 = one workgroup per plane).
 // req: 0 auto, -1 per plane, > 0 forced.  A range of R rows touches at most ceil(R/H) + 1
 // planes, so R <= 3H keeps it within SP_MAXSEG = 4 segments: G >= ceil(P/3).
@@ -135,14 +145,16 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
         int rc;
         if (a.tile_r > 0) {
             const int grid = P * s.nbands * s.st_nsegs;
-            s.par_redo = grid <= device_cus() ? 1 : 0;
+            const bool gen = !(s.ldw == s.W && s.st_nsegs == 1);
+            s.par_redo = grid_resident(grid, tile_blocks_per_cu(s, EXACT, ALPHA1, gen)) ? 1 : 0;
             if (!s.par_redo) return 0;   // (the tile kernel's finaliser recomputed stopped chains itself)
-            if (!launch_tile(s, dim3(grid), st, EXACT, ALPHA1, !(s.ldw == s.W && s.st_nsegs == 1)))
+            if (!launch_tile(s, dim3(grid), st, EXACT, ALPHA1, gen))
                 return fail(0, "psgla_tv_step: internal error: no tile kernel of this shape");
             rc = launch_check("tv_tile_kernel(redo)");
         } else {
             const int grid = s.split_wgs > 0 ? s.split_wgs : s.st_nvp;
-            s.par_redo = grid <= device_cus() ? 1 : 0;
+            s.par_redo = grid_resident(grid, stream_blocks_per_cu(EXACT, ALPHA1, !(s.ldw == s.W && s.st_nsegs == 1),
+                                                                  s.st_half != 0)) ? 1 : 0;
             if (!s.par_redo) return 0;
             launch_stream(s, dim3(grid), st, EXACT, ALPHA1, !(s.ldw == s.W && s.st_nsegs == 1), s.st_half != 0);
             rc = launch_check("tv_stream_kernel(redo)");
@@ -164,8 +176,8 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
             if (s.norm_copies < 1 || s.C * s.nbands * s.st_nsegs < 64) s.norm_copies = 1;
             // parallel early-stop redo when every tile is resident at once (its grid barrier); otherwise the
             // finalising workgroup recomputes stopped chains itself
-            s.par_redo = (s.redo && grid <= device_cus()) ? 1 : 0;
             const bool gen = !(s.ldw == s.W && s.st_nsegs == 1);
+            s.par_redo = (s.redo && grid_resident(grid, tile_blocks_per_cu(s, EXACT, ALPHA1, gen))) ? 1 : 0;
             if (launch_tile(s, dim3(grid), st, EXACT, ALPHA1, gen)) return launch_check("tv_tile_kernel");
             return fail(0, "psgla_tv_step: internal error: no tile kernel of this shape");
         }
@@ -173,8 +185,8 @@ static int launch_tv(const TvArgs& a, hipStream_t st, int mask = 3) {
             TvArgs s = a;
             s.fin_inline = (mask & 2) ? 1 : 0;
             const int grid = s.split_wgs > 0 ? s.split_wgs : s.st_nvp;   // virtual planes
-            s.par_redo = (s.redo && grid <= device_cus()) ? 1 : 0;         // (one workgroup per CU: LDS)
             const bool gen = !(s.ldw == s.W && s.st_nsegs == 1);
+            s.par_redo = (s.redo && grid_resident(grid, stream_blocks_per_cu(EXACT, ALPHA1, gen, s.st_half != 0))) ? 1 : 0;
             launch_stream(s, dim3(grid), st, EXACT, ALPHA1, gen, s.st_half != 0);
             int rc = launch_check("tv_stream_kernel");
             if (rc) return rc;

@@ -349,5 +349,19 @@ template <bool EXACT, int FRONT, bool ALPHA1> void launch_band_main(const TvArgs
 template <bool EXACT, int FRONT, bool ALPHA1> void launch_band_finalise(const TvArgs& a, dim3 grid, hipStream_t st);
 void launch_stream(const TvArgs& a, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen, bool half);
 bool launch_tile(const TvArgs& a, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen);
+// workgroups of the instance launch_stream / launch_tile would run that one CU holds at once (the runtime's occupancy
+// query, cached per instance; 0 if unknown): the parallel early-stop redo's grid barrier needs the grid resident
+int stream_blocks_per_cu(bool exact, bool alpha1, bool gen, bool half);
+int tile_blocks_per_cu(const TvArgs& a, bool exact, bool alpha1, bool gen);
+
+// cached hipOccupancyMaxActiveBlocksPerMultiprocessor of one kernel instance (slot: the instance's index)
+static inline int occupancy_cached(int* cache, int slot, const void* kernel, int threads) {
+    if (cache[slot] < 0) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, threads, 0) != hipSuccess) n = 0;
+        cache[slot] = n;
+    }
+    return cache[slot];
+}
 
 }  // namespace psgla

@@ -974,6 +974,19 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
     }
 }
 
+int stream_blocks_per_cu(bool exact, bool alpha1, bool gen, bool half) {
+    static int cache[16] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+    const int slot = (exact ? 8 : 0) | (alpha1 ? 4 : 0) | (gen ? 2 : 0) | (half ? 1 : 0);
+#define PSGLA_STREAM_OCC(E, A, G, HF) \
+    if (exact == E && alpha1 == A && gen == G && half == HF) \
+        return occupancy_cached(cache, slot, reinterpret_cast<const void*>(&tv_stream_kernel<E, A, G, HF>), TV_THREADS);
+    PSGLA_STREAM_OCC(true, true, false, false) PSGLA_STREAM_OCC(true, true, true, false) PSGLA_STREAM_OCC(true, false, false, false) PSGLA_STREAM_OCC(true, false, true, false)
+    PSGLA_STREAM_OCC(false, true, false, false) PSGLA_STREAM_OCC(false, true, true, false) PSGLA_STREAM_OCC(false, false, false, false) PSGLA_STREAM_OCC(false, false, true, false)
+    PSGLA_STREAM_OCC(true, true, true, true) PSGLA_STREAM_OCC(true, false, true, true) PSGLA_STREAM_OCC(false, true, true, true) PSGLA_STREAM_OCC(false, false, true, true)
+#undef PSGLA_STREAM_OCC
+    return 0;
+}
+
 void launch_stream(const TvArgs& s, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen, bool half) {
 #define PSGLA_STREAM(E, A, G, HF) \
     if (exact == E && alpha1 == A && gen == G && half == HF) { hipLaunchKernelGGL((tv_stream_kernel<E, A, G, HF>), grid, dim3(TV_THREADS), 0, st, s); return; }

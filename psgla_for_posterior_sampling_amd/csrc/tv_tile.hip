@@ -572,6 +572,19 @@ __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
     }
 }
 
+int tile_blocks_per_cu(const TvArgs& s, bool exact, bool alpha1, bool gen) {
+    static int cache[16] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+    const int slot = (exact ? 8 : 0) | (alpha1 ? 4 : 0) | (gen ? 2 : 0) | (s.tile_r == 3 ? 1 : 0);
+#define PSGLA_TILE_OCC(E, A, NWV, RV) \
+    if (exact == E && alpha1 == A && s.tile_nw == NWV && s.tile_r == RV) \
+        return occupancy_cached(cache, slot, gen ? reinterpret_cast<const void*>(&tv_tile_kernel<E, A, RV, true, NWV>) \
+                                                 : reinterpret_cast<const void*>(&tv_tile_kernel<E, A, RV, false, NWV>), NWV * WAVE);
+    PSGLA_TILE_OCC(true, true, 16, 2) PSGLA_TILE_OCC(true, false, 16, 2) PSGLA_TILE_OCC(false, true, 16, 2) PSGLA_TILE_OCC(false, false, 16, 2)
+    PSGLA_TILE_OCC(true, true, 16, 3) PSGLA_TILE_OCC(false, true, 16, 3)
+#undef PSGLA_TILE_OCC
+    return 0;
+}
+
 bool launch_tile(const TvArgs& s, dim3 grid, hipStream_t st, bool exact, bool alpha1, bool gen) {
 #define PSGLA_TILE(E, A, NWV, RV) \
     if (exact == E && alpha1 == A && s.tile_nw == NWV && s.tile_r == RV) { \
