@@ -76,6 +76,11 @@ def budget(L):
     return ph, end
 
 
+if os.environ.get("TDIAG_CLOCK"):                # tools/patches/tile_clock.py: shader ticks over the iterations
+    for L, nm in ((A, "launch_k-1"), (Bq, "launch_k")):
+        work = L[:, 1] > 0
+        ghz = L[work, 7] / ((L[work, 3] - L[work, 2]) * 10.0)
+        print(f"shader clock over the iterations ({nm}): mean {ghz.mean():.3f} GHz, min {ghz.min():.3f}, max {ghz.max():.3f}")
 pa, endA = budget(A)
 pb, _ = budget(Bq)
 gap = us(Bq[:, 0].min() - endA)
