@@ -220,6 +220,12 @@ static int check_tv_common(int B, int C, int H, int W, int n_tv) {
 // ldw and n_tv of `a` set): 0 band kernel (+ finaliser), 1 row stream, 3 small-batch tile kernel; -1 with
 // g_sel_err on a shape the requested variant does not support.
 static thread_local const char* g_sel_err = "";
+// The fast kernels are compiled for deepinv's TV constants (literal operands, psgla_common.hpp TV_*); a fast request
+// with other constants runs the exact kernels (correct at any constants, slower)
+static bool tv_fast_constants(const TvArgs& a) {
+    return a.tau == TV_TAU && a.opt == TV_OPT && a.sig_tv == TV_SIG && a.rho == TV_RHO && a.inv_opt == TV_INV_OPT;
+}
+
 static int select_step_kernel(const PsglaTvStep* d, TvArgs& a) {
     a.halo = d->n_tv;
     tv_tiling(a);
@@ -357,7 +363,7 @@ int psgla_tv_step(const PsglaTvStep* d, const PsglaSchedule* s, void* stream) {
     if (select_step_kernel(d, a) < 0) return g_sel_err == g_err ? (int)hipErrorInvalidValue : fail(0, g_sel_err);
     hipStream_t st = (hipStream_t)stream;
     const int m = d->launch_mask;
-    if (d->exact)
+    if (d->exact || !tv_fast_constants(a))
         return alpha1 ? launch_tv<true, FRONT_INPAINT, true>(a, st, m) : launch_tv<true, FRONT_INPAINT, false>(a, st, m);
     return alpha1 ? launch_tv<false, FRONT_INPAINT, true>(a, st, m) : launch_tv<false, FRONT_INPAINT, false>(a, st, m);
 }
@@ -397,7 +403,8 @@ int psgla_tv_prox(const PsglaTvProx* d, void* stream) {
     a.halo = d->n_tv;
     tv_tiling(a);
     hipStream_t st = (hipStream_t)stream;
-    return d->exact ? launch_tv<true, FRONT_GIVEN, true>(a, st) : launch_tv<false, FRONT_GIVEN, true>(a, st);
+    return (d->exact || !tv_fast_constants(a)) ? launch_tv<true, FRONT_GIVEN, true>(a, st)
+                                               : launch_tv<false, FRONT_GIVEN, true>(a, st);
 }
 
 }  // extern "C"

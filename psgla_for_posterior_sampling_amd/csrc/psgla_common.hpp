@@ -77,6 +77,19 @@ constexpr int MAXIT = PSGLA_TV_MAX_FUSED_IT;
 constexpr int MAXG = 1024;        // chains per launch (early-stop groups)
 constexpr uint32_t TAG_LANGEVIN = 0;
 
+// deepinv 0.2.1 TVDenoiser's step constants (tau = 0.01, rho = 1.99, sigma = 1 / tau / 8: fixed by
+// /root/reference/sampling_images.py:138, which never passes others) in fp32, as the FAST kernels' compile-time
+// operands.  Round 6 (tools/valu_probe2, profiles/r06q_valu_probe.txt): at 4 waves per SIMD a VALU instruction
+// with an SGPR source costs 4.24-4.30 SIMD cycles per wave-instruction, one with a literal (v_fmamk_f32,
+// VOP2 literal) 2.57 whatever the VGPR banks of the others, VGPR-only 2.17 / 2.57 (VOP2 / VOP3) unless two of three
+// sources share a bank (4.24-4.39).  A fast request with other constants runs the exact kernels (api.hip:
+// tv_fast_constants) -- the fast arithmetic, and so every fast result, is unchanged.
+constexpr float TV_TAU = 0x1.47ae14p-7f;       // fp32(0.01)
+constexpr float TV_OPT = 0x1.028f5cp+0f;       // fp32(1 + 0.01)
+constexpr float TV_INV_OPT = 0x1.faee42p-1f;   // fp32(1 / (double)fp32(1.01)), TvArgs::inv_opt
+constexpr float TV_SIG = 12.5f;                // fp32(1 / 0.01 / 8)
+constexpr float TV_RHO = 0x1.fd70a4p+0f;       // fp32(1.99)
+
 enum Front { FRONT_INPAINT = 0, FRONT_GIVEN = 1 };
 
 struct TvArgs {
@@ -199,6 +212,21 @@ __device__ __forceinline__ float wave_sum(float v) {
     return (r0 + r1) + (r2 + r3);
 }
 // Sums over each 16-lane row, returned in every lane of the row (the first 4 steps of wave_sum).
+// A kernel constant (an SGPR) copied once into a VGPR for 2-source VALU operands (4.24 -> 2.17 SIMD cycles per
+// wave-instruction at 4 waves per SIMD, above); non-volatile asm, so it is CSE'd and hoisted out of loops
+__device__ __forceinline__ float vconst(float s) {
+    float v;
+    asm("v_mov_b32 %0, %1" : "=v"(v) : "s"(s));
+    return v;
+}
+
+// the TV dual's projection factor min(1, ths / |v|) = min(1, ths * rsq(s2)) as one multiply with the clamp
+// modifier (fminf(fmaxf(x, 0), 1) folds to v_mul_f32_e64 ... clamp): identical for x >= 0 and +inf, and no v_min
+// (4.24 SIMD cycles per wave-instruction at 4 waves per SIMD)
+__device__ __forceinline__ float tv_proj_factor(float ths_v, float s2) {
+    return fminf(fmaxf(ths_v * __builtin_amdgcn_rsqf(s2), 0.0f), 1.0f);
+}
+
 __device__ __forceinline__ float2 row_sum2(float a, float b) {
     a += PSGLA_DPP(a, 0xB1); b += PSGLA_DPP(b, 0xB1);      // quad_perm [1,0,3,2]
     a += PSGLA_DPP(a, 0x4E); b += PSGLA_DPP(b, 0x4E);      // quad_perm [2,3,0,1]

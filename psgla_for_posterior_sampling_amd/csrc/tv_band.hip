@@ -187,9 +187,9 @@ __device__ __forceinline__ void tv_tile(const TvArgs& a, int plane, int tile, in
                     zv = 2.0f * xv - xo;
                     xn = xo + a.rho * (xv - xo);
                 } else {
-                    xv = __builtin_fmaf(a.tau, f4get(yrow, k) - t, xo) * a.inv_opt;
+                    xv = __builtin_fmaf(TV_TAU, f4get(yrow, k) - t, xo) * TV_INV_OPT;
                     zv = __builtin_fmaf(2.0f, xv, -xo);
-                    xn = __builtin_fmaf(a.rho, xv - xo, xo);
+                    xn = __builtin_fmaf(TV_RHO, xv - xo, xo);
                 }
                 if (trk) {
                     const bool core = colcore[k] && gi[r] >= r0 && gi[r] < r1;
@@ -231,12 +231,12 @@ __device__ __forceinline__ void tv_tile(const TvArgs& a, int plane, int tile, in
                     u0[r][k] = uo0 + a.rho * (n0 - uo0);
                     u1[r][k] = uo1 + a.rho * (n1 - uo1);
                 } else {
-                    const float v0 = __builtin_fmaf(a.sig_tv, g0, uo0);
-                    const float v1 = __builtin_fmaf(a.sig_tv, g1, uo1);
+                    const float v0 = __builtin_fmaf(TV_SIG, g0, uo0);
+                    const float v1 = __builtin_fmaf(TV_SIG, g1, uo1);
                     const float s2 = __builtin_fmaf(v0, v0, v1 * v1);
-                    const float f = fminf(1.0f, a.ths * __builtin_amdgcn_rsqf(s2));
-                    u0[r][k] = __builtin_fmaf(a.rho, __builtin_fmaf(v0, f, -uo0), uo0);
-                    u1[r][k] = __builtin_fmaf(a.rho, __builtin_fmaf(v1, f, -uo1), uo1);
+                    const float f = tv_proj_factor(vconst(a.ths), s2);
+                    u0[r][k] = __builtin_fmaf(TV_RHO, __builtin_fmaf(v0, f, -uo0), uo0);
+                    u1[r][k] = __builtin_fmaf(TV_RHO, __builtin_fmaf(v1, f, -uo1), uo1);
                 }
             }
         }

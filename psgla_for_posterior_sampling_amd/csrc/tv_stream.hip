@@ -271,9 +271,10 @@ __device__ __forceinline__ void stage_phase_a(const TvArgs& a, const float4& X2,
             zv = 2.0f * xv - xo;
             xn = xo + a.rho * (xv - xo);
         } else {
-            xv = __builtin_fmaf(a.tau, yy[kk] - tt, xo) * a.inv_opt;
+            // deepinv's constants as literal operands (psgla_common.hpp TV_*: fast kernels run only for them)
+            xv = __builtin_fmaf(TV_TAU, yy[kk] - tt, xo) * TV_INV_OPT;
             zv = __builtin_fmaf(2.0f, xv, -xo);
-            xn = __builtin_fmaf(a.rho, xv - xo, xo);
+            xn = __builtin_fmaf(TV_RHO, xv - xo, xo);
         }
         if (TRK) {
             // padded rows (GEN): the lane's columns >= W are not part of the image's norms
@@ -323,12 +324,12 @@ __device__ __forceinline__ void stage_phase_b(const TvArgs& a, const StageRow& r
             un0[kk] = uo0 + a.rho * (v0 / dd - uo0);
             un1[kk] = uo1 + a.rho * (v1 / dd - uo1);
         } else {
-            const float v0 = __builtin_fmaf(a.sig_tv, g0, uo0);
-            const float v1 = __builtin_fmaf(a.sig_tv, g1, uo1);
+            const float v0 = __builtin_fmaf(TV_SIG, g0, uo0);
+            const float v1 = __builtin_fmaf(TV_SIG, g1, uo1);
             const float s2 = __builtin_fmaf(v0, v0, v1 * v1);
-            const float f = fminf(1.0f, a.ths * __builtin_amdgcn_rsqf(s2));
-            un0[kk] = __builtin_fmaf(a.rho, __builtin_fmaf(v0, f, -uo0), uo0);
-            un1[kk] = __builtin_fmaf(a.rho, __builtin_fmaf(v1, f, -uo1), uo1);
+            const float f = tv_proj_factor(vconst(a.ths), s2);
+            un0[kk] = __builtin_fmaf(TV_RHO, __builtin_fmaf(v0, f, -uo0), uo0);
+            un1[kk] = __builtin_fmaf(TV_RHO, __builtin_fmaf(v1, f, -uo1), uo1);
         }
     }
 }

@@ -152,7 +152,7 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
     // instead of a select per element and iteration (the same value: sigma * finite == 0 there)
     float sg1[CPL];
 #pragma unroll
-    for (int k = 0; k < CPL; ++k) sg1[k] = (GEN ? lastk == k : (k == CPL - 1 && lastlane)) ? 0.f : a.sig_tv;
+    for (int k = 0; k < CPL; ++k) sg1[k] = (GEN ? lastk == k : (k == CPL - 1 && lastlane)) ? 0.f : TV_SIG;
     // Trapezoid: the core rows need iteration j (1-based) only on rows [r0 - (n_it - j), r1 + (n_it - j))
     // for the dual and one row more below for the primal (the dual of a row reads the next row's z);
     // a wave none of whose rows is needed skips the phase (its stale rows feed only unneeded rows).
@@ -243,9 +243,10 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
                     zv = 2.0f * xv - xo;
                     xn = xo + a.rho * (xv - xo);
                 } else {
-                    xv = __builtin_fmaf(a.tau, yv[r][k] - tt, xo) * a.inv_opt;
+                    // deepinv's constants as literal operands (psgla_common.hpp TV_*; round 6)
+                    xv = __builtin_fmaf(TV_TAU, yv[r][k] - tt, xo) * TV_INV_OPT;
                     zv = __builtin_fmaf(2.0f, xv, -xo);
-                    xn = __builtin_fmaf(a.rho, xv - xo, xo);
+                    xn = __builtin_fmaf(TV_RHO, xv - xo, xo);
                 }
                 // rel-err terms of the counted rows (row-uniform test; lanes past W are masked once, at
                 // the reduction: adding nothing and adding +0 leave a lane's sum identical).  Fast mode (round 5):
@@ -293,6 +294,8 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
             const bool down = gi[r] < H - 1;
             // fast mode (round 5): the plane's last row (no vertical difference) takes sigma 0 in its dual -- a
             // row-uniform scalar instead of a per-element select (the same value: sigma * 0 == 0 * finite)
+            // (a.sig_tv == TV_SIG in the fast mode; a select between the literal and 0 made the register allocator
+            // spill a VGPR in the 48-row instance, round 6)
             const float sg0 = down ? a.sig_tv : 0.f;
 #pragma unroll
             for (int k = 0; k < CPL; ++k) {
@@ -315,9 +318,9 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
                     const float v0 = __builtin_fmaf(sg0, zd - zc, uo0);
                     const float v1 = __builtin_fmaf(sg1[k], zr - zc, uo1);
                     const float s2 = __builtin_fmaf(v0, v0, v1 * v1);
-                    const float f = fminf(1.0f, a.ths * __builtin_amdgcn_rsqf(s2));
-                    u0[r][k] = __builtin_fmaf(a.rho, __builtin_fmaf(v0, f, -uo0), uo0);
-                    u1[r][k] = __builtin_fmaf(a.rho, __builtin_fmaf(v1, f, -uo1), uo1);
+                    const float f = tv_proj_factor(vconst(a.ths), s2);
+                    u0[r][k] = __builtin_fmaf(TV_RHO, __builtin_fmaf(v0, f, -uo0), uo0);
+                    u1[r][k] = __builtin_fmaf(TV_RHO, __builtin_fmaf(v1, f, -uo1), uo1);
                 }
             }
         }
