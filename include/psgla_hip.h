@@ -110,7 +110,9 @@ typedef struct PsglaTvStep {
     float alpha;              /* relaxation (:238)                                        */
     float tau, one_plus_tau, sigma_tv, rho, ths, tol;  /* TVDenoiser constants (fp32)     */
     int32_t n_tv;             /* inner iterations n_it_max (<= PSGLA_TV_MAX_FUSED_IT)     */
-    int32_t exact;            /* 1: reference op order + IEEE div/sqrt (bit-exact checker mode) */
+    int32_t exact;            /* 1: reference op order + IEEE div/sqrt (bit-exact checker mode);
+                                 0 (fast) runs the fast kernels only for deepinv's TV constants
+                                 (tau 0.01, rho 1.99, sigma 1/(8 tau) in fp32): others take the exact ones */
     uint64_t seed;            /* seed_alg                                                 */
     int32_t chain0;           /* global id of chain 0 of this batch (multi-GPU sharding)  */
     int32_t advance_step;     /* 1: finaliser increments *d_step                           */

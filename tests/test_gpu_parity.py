@@ -348,6 +348,36 @@ def test_fused_full_size_fast_vs_exact():
     assert rel(xf.cpu().numpy(), xe.cpu().numpy()) < 1e-4
 
 
+@pytest.mark.parametrize("variant", ["stream", "tile", "band"])
+def test_fast_request_with_other_tv_constants_runs_exact(variant):
+    """Round 6: the fast kernels are compiled for deepinv's TV constants (literal operands); a fast
+    request with other constants (tau = 0.02, rho = 1.5) must run the exact kernels -- bit-identical to an exact
+    request -- and the default constants keep the fast path (it differs from exact in the last bits)."""
+    from psgla_for_posterior_sampling_amd.engine import FusedTvChains
+    from psgla_for_posterior_sampling_amd import hip_ops as K
+    g = torch.Generator(device=DEV).manual_seed(321)
+    x = torch.rand((1, 3, 64, 64), generator=g, device=DEV)
+    from psgla_for_posterior_sampling_amd.fidelity import inpainting_problem
+    dg, y, init, mask2d, _ = inpainting_problem(x)
+    c1, c2 = orc.psgla_coefficients((10 / 255.0) ** 2, 10.0, 10 / 255.0)
+
+    def run(exact, tau, rho):
+        eng = FusedTvChains(init.expand(4, -1, -1, -1).contiguous(), y, dg.mask_u8, c1=c1, c2=c2,
+                            sigma2=dg.sigma2, alpha=1.0, ths=float(np.float32(10 / 255.0)),
+                            tv=K.TvConstants(tau=tau, rho=rho, n_it_max=10), seed=0, n_iter=6, n_inter=3,
+                            n_inter_mmse=2, exact=exact, kernel_variant=variant)
+        eng.run(6, graph_steps=0)
+        torch.cuda.synchronize()
+        return eng.X.clone(), eng.u2_state.clone(), eng.blocks()[0].clone()
+
+    for a, b in zip(run(False, 0.02, 1.5), run(True, 0.02, 1.5)):
+        assert torch.equal(a, b)
+    xf, _, _ = run(False, 0.01, 1.99)
+    xe, _, _ = run(True, 0.01, 1.99)
+    assert not torch.equal(xf, xe), "default constants should take the fast kernels"
+    assert _relt(xf, xe) < 1e-4
+
+
 def _relt(a, b):
     return float(torch.linalg.vector_norm((a - b).double()) / torch.linalg.vector_norm(b.double()))
 
