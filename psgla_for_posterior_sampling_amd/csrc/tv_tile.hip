@@ -478,10 +478,35 @@ __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
     // ---- step finalisation by the last workgroup to arrive (as tv_stream_kernel) ----
     const int G = a.B;
     for (int g = threadIdx.x; g < G; g += blockDim.x) sh.s_stop[g] = 0;
+    // Few chains with several norm copies (the CLI's castle at batch 1-4: 8 copies): every (chain, iteration, copy)
+    // pair is read by its own thread -- two exchanges per lane, issued by a few wave-instructions -- into LDS
+    // (sh.red is free here), then summed in copy order by one thread per (chain, iteration): the same sums as the
+    // per-(chain, iteration) loop below, whose 16 exchanges per lane issue one after another (round 6)
+    const int ncp = a.norm_copies;
+    constexpr int RED_D = (int)(sizeof(sh.red) / sizeof(double));
+    const bool spread = ncp > 1 && ncp <= 8 && G * MAXIT * ncp * 2 <= RED_D;
+    double* const cpv = reinterpret_cast<double*>(&sh.red[0][0][0]);
+    if (spread) {
+        const size_t cstride = (size_t)a.B * a.n_tv * 2;
+        for (int i = threadIdx.x; i < G * MAXIT * ncp; i += blockDim.x) {
+            const int gt = i / ncp, cp = i - gt * ncp;
+            const int g = gt / MAXIT, t = gt - g * MAXIT;
+            if (t >= trk_lo(a) && t <= trk_hi(a) && t < a.n_tv) {
+                double* const n0 = a.norms + (size_t)cp * cstride + ((size_t)g * a.n_tv + t) * 2;
+                cpv[2 * i] = __hip_atomic_exchange(n0, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                cpv[2 * i + 1] = __hip_atomic_exchange(n0 + 1, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
     __syncthreads();
     for (int i = threadIdx.x; i < G * MAXIT; i += blockDim.x) {
         const int g = i / MAXIT, t = i - g * MAXIT;
-        if (t >= trk_lo(a) && t <= trk_hi(a) && t < a.n_tv) {
+        if (spread && t >= trk_lo(a) && t <= trk_hi(a) && t < a.n_tv) {
+            double nd = 0.0, nn = 0.0;
+            for (int cp = 0; cp < ncp; ++cp) { nd += cpv[2 * (i * ncp + cp)]; nn += cpv[2 * (i * ncp + cp) + 1]; }
+            const float rel = (float)sqrt(nd) / (float)sqrt(nn);
+            if (rel < a.tol) atomicOr(&sh.s_stop[g], 1 << t);
+        } else if (!spread && t >= trk_lo(a) && t <= trk_hi(a) && t < a.n_tv) {
             // read by agent-scope atomics (exchange with 0.0: read and reset in one operation), as they were
             // written: 8-B agent atomics on both sides of the hand-off, performed where the producers' adds were
             // With several copies, the first 8 copies' reads are issued back to back and waited for once (round 4:

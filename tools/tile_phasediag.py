@@ -81,6 +81,11 @@ if os.environ.get("TDIAG_CLOCK"):                # tools/patches/tile_clock.py: 
         work = L[:, 1] > 0
         ghz = L[work, 7] / ((L[work, 3] - L[work, 2]) * 10.0)
         print(f"shader clock over the iterations ({nm}): mean {ghz.mean():.3f} GHz, min {ghz.min():.3f}, max {ghz.max():.3f}")
+if os.environ.get("TDIAG_FIN7"):                 # tools/patches/tile_fin_stamp.py: stamp 7 after the norms exchange
+    for L, nm in ((A, "launch_k-1"), (Bq, "launch_k")):
+        fin = int(np.argmax(L[:, 6]))
+        print(f"finaliser ({nm}): arrival -> norms read {us(L[fin, 7] - L[fin, 5]):.2f} us, "
+              f"-> end {us(L[fin, 6] - L[fin, 7]):.2f} us")
 pa, endA = budget(A)
 pb, _ = budget(Bq)
 gap = us(Bq[:, 0].min() - endA)
