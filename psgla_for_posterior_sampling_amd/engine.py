@@ -317,7 +317,10 @@ class FusedTvChains:
         return self._view(self.sched.blocks[:k]), self._view(self.sched.blocks2[:k])
 
     def lists(self):
-        """The reference's return value: lists of squeezed (C, H, W) tensors (views of the stores)."""
+        """The reference's return value: lists of squeezed (C, H, W) tensors (views of the stores).  Checks the
+        early-stop hand-off guard first (check_handoff: settles, one host sync -- the results are being read;
+        ADVICE r5: not only in psgla())."""
+        self.check_handoff()
         ns = self.sched.n_samples_done(self.steps_done)
         nb = self.sched.n_blocks_done(self.steps_done)
         sm, (b1, b2) = self.samples(), self.blocks()
