@@ -88,6 +88,25 @@ FORMS = {
                                                     f"v_cndmask_b32_e64 v{ACC[4 * j + 2]}, v2, v1, s[40:41]",
                                                     f"v_cndmask_b32_e64 v{ACC[4 * j + 3]}, v1, v{ACC[4 * j + 3]}, s[40:41]")],
     "cnd_vcc_after_cmp": ["v_cmp_gt_f32 vcc, v1, v2"] + blk(lambda i: f"v_cndmask_b32 v{ACC[i]}, v1, v{ACC[i]}, vcc")[:15],
+    # one compare + one select among 14 independent adds: the marginal price of a select reading VCC (e32) or an
+    # SGPR pair (e64), against the same block with an add in the select's place
+    "mix_cnd_vcc":   ["v_cmp_gt_f32 vcc, v1, v2"] + [f"v_add_f32 v{ACC[i]}, v1, v{ACC[i]}" for i in range(7)] +
+                     ["v_cndmask_b32 v5, v1, v2, vcc"] + [f"v_add_f32 v{ACC[i]}, v1, v{ACC[i]}" for i in range(7, 14)],
+    "mix_cnd_s":     ["v_cmp_gt_f32_e64 s[40:41], v1, v2"] + [f"v_add_f32 v{ACC[i]}, v1, v{ACC[i]}" for i in range(7)] +
+                     ["v_cndmask_b32_e64 v5, v1, v2, s[40:41]"] + [f"v_add_f32 v{ACC[i]}, v1, v{ACC[i]}" for i in range(7, 14)],
+    "mix_add":       ["v_cmp_gt_f32 vcc, v1, v2"] + [f"v_add_f32 v{ACC[i]}, v1, v{ACC[i]}" for i in range(7)] +
+                     ["v_add_f32 v5, v1, v2"] + [f"v_add_f32 v{ACC[i]}, v1, v{ACC[i]}" for i in range(7, 14)],
+    "mix_nocmp":     [f"v_add_f32 v{ACC[i]}, v1, v{ACC[i]}" for i in range(16)],
+    # integer forms of the Philox rounds (round 6): 32x32 -> 64 multiply-add, high half, xors with an SGPR key
+    "mad_u64_vv":    [f"v_mad_u64_u32 v[{ACC0[i % 8]}:{ACC0[i % 8] + 1}], s[42:43], v{B1[i % 8]}, v2, 0" for i in range(16)],
+    "mad_u64_sv":    [f"v_mad_u64_u32 v[{ACC0[i % 8]}:{ACC0[i % 8] + 1}], s[42:43], %1, v{B1[i % 8]}, 0" for i in range(16)],
+    "mul_hi_vv":     blk(lambda i: f"v_mul_hi_u32 v{ACC[i]}, v{B1[i % 8]}, v2"),
+    "mul_hi_sv":     blk(lambda i: f"v_mul_hi_u32 v{ACC[i]}, %1, v{B1[i % 8]}"),
+    "mul_lo_vv":     blk(lambda i: f"v_mul_lo_u32 v{ACC[i]}, v{B1[i % 8]}, v2"),
+    "xor_vv":        blk(lambda i: f"v_xor_b32 v{ACC[i]}, v1, v{ACC[i]}"),
+    "xor_sv":        blk(lambda i: f"v_xor_b32 v{ACC[i]}, %1, v{ACC[i]}"),
+    "sqrt":          blk(lambda i: f"v_sqrt_f32 v{ACC[i]}, v1"),
+    "cvt_f32_u32":   blk(lambda i: f"v_cvt_f32_u32 v{ACC[i]}, v{B1[i % 8]}"),
     # transcendental and data movement
     "rsq":           blk(lambda i: f"v_rsq_f32 v{ACC[i]}, v1"),
     "mov_dpp":       blk(lambda i: f"v_mov_b32_dpp v{ACC[i]}, v1 row_shr:1 row_mask:0xf bank_mask:0xf"),
@@ -103,7 +122,7 @@ FORMS = {
 
 
 def hip_src():
-    clob = ", ".join(f'"v{r}"' for r in range(1, 64)) + ', "s40", "s41", "vcc"' 
+    clob = ", ".join(f'"v{r}"' for r in range(1, 64)) + ', "s40", "s41", "s42", "s43", "vcc"' 
     init = " ".join(f"v_mov_b32 v{r}, 0.5\\n" for r in range(1, 64))
     out = ['// generated by tools/valu_probe_gen.py -- VALU issue cost by operand form (diagnostic)',
            '#include <hip/hip_runtime.h>', '#include <cstdio>', '#include <cstdlib>', '#include <vector>', '']
