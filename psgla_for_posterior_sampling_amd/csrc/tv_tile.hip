@@ -31,6 +31,8 @@ struct TileShared {
     float2 red[MAXIT][NW][4];          // rel_err partial sums per (iteration, wave, 16-lane row of the wave)
     int s_stop[MAXG];
     int s_flag, s_item, s_next;
+    int s_uncert;                      // this tile's rel-err partials do not rule out a stop (below)
+    int s_nuncert;                     // finaliser: tiles whose partials do not rule out a stop
 };
 
 // before_u2: called by every wave once the tile's rel-err sums and X side are issued, before its u2 stores
@@ -352,6 +354,12 @@ __device__ __forceinline__ void sb_tile(const TvArgs& a, TileShared<R, NW>& sh, 
             for (int ww = 0; ww < NW; ++ww)
                 for (int q = 0; q < 4; ++q) { sd += sh.red[t][ww][q].x; sn += sh.red[t][ww][q].y; }
             if (!EXACT) sd *= (double)(a.rho * a.rho);     // fast sums hold (x - x2_prev)^2
+            // Round 6: deepinv stops when ||x2 - x2_prev|| < tol ||x2||, i.e. sum(d) < tol^2 sum(n) over the chain's
+            // tiles.  A tile whose own partials satisfy d >= tol^2 (1 + 1e-5) n cannot contribute to a stop; when no
+            // tile of the launch reports otherwise (the arrival count's high half), the finaliser knows that no chain
+            // stopped without reading the sums (the 1e-5 margin covers the fp64 sums and the fp32 sqrt / divide of
+            // the test, whose rounding is below 1e-6 relative)
+            if (!(sd >= ((double)a.tol * (double)a.tol) * (1.0 + 1e-5) * sn)) sh.s_uncert = 1;
             // workgroup x adds to copy x % norm_copies (x & 7 = its XCD when there are 8): fewer adds queue
             // on one address when many tiles share a chain
             double* const nc = nrm + (size_t)(blockIdx.x % a.norm_copies) * ((size_t)a.B * a.n_tv * 2);
@@ -402,6 +410,7 @@ __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
     constexpr bool SPLIT = NW == 8;                    // two-phase arrival (below)
     const long long step = launch_step(a);
     const bool fresh = launch_fresh(a);
+    if (threadIdx.x == 0) sh.s_uncert = 0;             // (read after sb_tile's barriers)
     const int P = a.B * a.C;
     const int T = a.nbands * (GEN ? a.st_nsegs : 1);  // tiles per plane: (column segment, band)
     {
@@ -451,8 +460,11 @@ __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
         // agent atomics (MI355X_MICROARCH.md: "8-B agent atomics both sides" with its hand-off row 1; a
         // release + acquire pair cost 1.1 us per step here).  Nothing else this launch wrote is read by it
         // (the rare redo reads the step's inputs, written by the previous launch).
-                const int old = __hip_atomic_fetch_add(a.arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // (one-phase arrival: the high half counts the tiles whose rel-err partials leave a stop possible)
+                const int unc = SPLIT ? 0 : (sh.s_uncert ? 1 : 0);
+                const int old = __hip_atomic_fetch_add(a.arrive, 1 + (unc << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 sh.s_flag = ((old & 0xFFFF) == (int)gridDim.x - 1) ? 1 : 0;
+                sh.s_nuncert = SPLIT ? 1 : (old >> 16) + unc;
             }
             wait_vm0();
             __syncthreads();
@@ -477,12 +489,34 @@ __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
     }
     // ---- step finalisation by the last workgroup to arrive (as tv_stream_kernel) ----
     const int G = a.B;
+    const int ncp = a.norm_copies;
+    // Round 6: no tile left a stop possible (its rel-err partials, above: the arrival count's high half) -- the common
+    // case -- so no chain stopped: the sums are only zeroed for the next step and the pending word cleared, by
+    // stores with no barrier after them (a __syncthreads waits for the stores before it: ~1 us)
+    if (sh.s_nuncert == 0) {
+        const size_t cstride = (size_t)a.B * a.n_tv * 2;
+        for (int i = threadIdx.x; i < G * MAXIT * ncp; i += blockDim.x) {
+            const int gt = i / ncp, cp = i - gt * ncp;
+            const int g = gt / MAXIT, t = gt - g * MAXIT;
+            if (t >= trk_lo(a) && t <= trk_hi(a) && t < a.n_tv) {
+                double* const n0 = a.norms + (size_t)cp * cstride + ((size_t)g * a.n_tv + t) * 2;
+                __hip_atomic_store(n0, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(n0 + 1, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if (a.par_redo && threadIdx.x == 0) {
+            a.redo[1] = 0;
+            a.redo[0] = 0;
+        }
+        // the stores complete before the resets below (measured: without this wait 8 chains +0.7 %, castle at batch 1
+        // -2.6 %; with it 0 % / -3.8 % against the full finalisation, profiles/r06ze_tile_nostop_ab.txt)
+        wait_vm0();
+    } else {
     for (int g = threadIdx.x; g < G; g += blockDim.x) sh.s_stop[g] = 0;
     // Few chains with several norm copies (the CLI's castle at batch 1-4: 8 copies): every (chain, iteration, copy)
     // pair is read by its own thread -- two exchanges per lane, issued by a few wave-instructions -- into LDS
     // (sh.red is free here), then summed in copy order by one thread per (chain, iteration): the same sums as the
     // per-(chain, iteration) loop below, whose 16 exchanges per lane issue one after another (round 6)
-    const int ncp = a.norm_copies;
     constexpr int RED_D = (int)(sizeof(sh.red) / sizeof(double));
     const bool spread = ncp > 1 && ncp <= 8 && G * MAXIT * ncp * 2 <= RED_D;
     double* const cpv = reinterpret_cast<double*>(&sh.red[0][0][0]);
@@ -587,8 +621,9 @@ __global__ void __launch_bounds__(NW * WAVE) tv_tile_kernel(const TvArgs a) {
         }
     }
     __syncthreads();
-    // (the norm copies were zeroed by the exchanges that read them; entries outside the tracked iterations are
-    // never written)
+    }
+    // (the norm copies were zeroed by the exchanges that read them, or by the stores above; entries outside the
+    // tracked iterations are never written)
     if (threadIdx.x == 0) {
         // both counts out (the other workgroups' phase-2 adds may still be landing: an add, not a store); the
         // counter is 0 once the kernel has completed

@@ -86,6 +86,10 @@ if os.environ.get("TDIAG_FIN7"):                 # tools/patches/tile_fin_stamp.
         fin = int(np.argmax(L[:, 6]))
         print(f"finaliser ({nm}): arrival -> norms read {us(L[fin, 7] - L[fin, 5]):.2f} us, "
               f"-> end {us(L[fin, 6] - L[fin, 7]):.2f} us")
+if os.environ.get("TDIAG_NUNC"):                 # tools/patches/tile_nuncert.py: tiles leaving a stop possible
+    for L, nm in ((A, "launch_k-1"), (Bq, "launch_k")):
+        fin = int(np.argmax(L[:, 6]))
+        print(f"finaliser ({nm}): {int(L[fin, 7])} of {G} tiles leave a stop possible")
 pa, endA = budget(A)
 pb, _ = budget(Bq)
 gap = us(Bq[:, 0].min() - endA)
