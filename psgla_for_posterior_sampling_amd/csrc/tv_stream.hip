@@ -895,13 +895,16 @@ __global__ void __launch_bounds__(TV_THREADS) tv_stream_kernel(const TvArgs a) {
         }
     }
     // ---- step finalisation by the last workgroup to arrive (no second launch) ----
-    // Every wave's stores and atomics complete, then one agent release per workgroup (writes the
-    // XCD's dirty L2 lines back), then the arrival count.  The last
-    // workgroup acquires before reading the rel-err sums or re-streaming a chain.
+    // Every wave's stores and atomics complete, then -- only when the finaliser may re-stream chains in this launch
+    // (the serial early-stop recompute, par_redo = 0) -- one agent release per workgroup (writes the XCD's dirty L2
+    // lines back), then the arrival count.  With the parallel redo nothing in this launch reads another
+    // workgroup's plain stores (the rel-err sums are agent atomics, complete at wait_vm0; the redo runs in the next
+    // launch, after the kernel boundary): round 6, -1.8 % at 64 chains, profiles/r06zh_stream_norelease_ab.txt.  The
+    // last workgroup acquires before reading the rel-err sums or re-streaming a chain.
     wait_vm0();
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (!a.par_redo) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         const int old = __hip_atomic_fetch_add(a.arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_flag = (old == (int)gridDim.x - 1) ? 1 : 0;
         if (s_flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
