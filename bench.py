@@ -52,8 +52,8 @@ sys.path.insert(0, REPO)
 METRIC = "Langevin steps/sec (3×256×256, batch=64) at 1/2/4/8 GPU; HBM GB/s vs roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # committed PMC summaries (tools/profile_round.sh + tools/pmc_summary.py) by dominant kernel
-PMC_PROFILES = {"tv_stream_kernel": os.path.join("profiles", "r06zg_pmc_tv_stream.json"),
-                "tv_tile_kernel": os.path.join("profiles", "r06zg_pmc_tv_tile.json")}
+PMC_PROFILES = {"tv_stream_kernel": os.path.join("profiles", "r06zi_pmc_tv_stream.json"),
+                "tv_tile_kernel": os.path.join("profiles", "r06zi_pmc_tv_tile.json")}
 
 
 def parse():
